@@ -1,0 +1,94 @@
+"""Pins the Python oracle (oracle/dl_oracle.py) against the reference's own test
+vectors, transcribed in tests/golden/ by tests/golden/make_golden.py."""
+from collections import Counter
+
+import pytest
+
+from oracle import dl_oracle as O
+from tests.golden_io import check_links, load, spans
+
+DL = load("dependency_linker.json")
+SN = load("span_node.json")
+TM = load("trace_merge.json")
+ST = load("storage_dependencies.json")
+
+
+@pytest.mark.parametrize("case", DL["cases"], ids=lambda c: c["name"])
+def test_dependency_linker(case):
+    log = []
+    linker = O.DependencyLinker(log)
+    for t in case["traces"]:
+        linker.put_trace(spans(t))
+    for msg in case["log_contains"]:
+        assert msg in log
+    if case["mode"] != "log":
+        check_links(linker.link(), case["expect"], case["mode"])
+
+
+@pytest.mark.parametrize("case", DL["merge_cases"], ids=lambda c: c["name"])
+def test_dependency_linker_merge(case):
+    from tests.golden_io import links
+    check_links(O.DependencyLinker.merge(links(case["links"])), case["expect"], case["mode"])
+
+
+def _node_index(span, inputs):
+    for i, s in enumerate(inputs):
+        if s == span:
+            return i
+    raise AssertionError(f"node span not among inputs: {span}")
+
+
+@pytest.mark.parametrize("case", SN["cases"], ids=lambda c: c["name"])
+def test_span_node(case):
+    inputs = spans(case["spans"])
+    log = []
+    root = O.SpanNodeBuilder(log).build(inputs)
+    if "root" in case:
+        if case["root"] is None:
+            assert root.span is None
+        else:
+            assert root.span == inputs[case["root"]]
+    if "first_child_of_root" in case:
+        assert root.children[0].span == inputs[case["first_child_of_root"]]
+    nodes = list(root.traverse())
+    for parent_i, child_is in case.get("children", []):
+        node = root if parent_i is None else next(n for n in nodes if n.span == inputs[parent_i])
+        got = [c.span for c in node.children]
+        assert got == [inputs[i] for i in child_is]
+    if "tree_size" in case:
+        assert len(nodes) == case["tree_size"]
+    if "log_exact" in case:
+        assert log == case["log_exact"]
+    if "traverse_any_order" in case:
+        assert Counter(n.span for n in nodes) == Counter(inputs[i] for i in case["traverse_any_order"])
+
+
+@pytest.mark.parametrize("case", TM["cases"], ids=lambda c: c["name"])
+def test_trace_merge(case):
+    inputs = spans(case["spans"])
+    out = O.trace_merge(inputs)
+    if case["mode"] == "trace_ids":
+        assert [s.trace_id for s in out] == case["expect"]
+    elif case["mode"] == "exact":
+        assert out == spans(case["expect"])
+    else:
+        assert Counter(out) == Counter(spans(case["expect"]))
+
+
+@pytest.mark.parametrize("case", ST["cases"], ids=lambda c: c["name"])
+def test_storage_get_dependencies(case):
+    store = O.InMemoryStorage(strict_trace_id=True)
+    for b in case["batches"]:
+        store.accept(spans(b))
+    for q in case["queries"]:
+        check_links(store.get_dependencies(q["endTs"], q["lookback"]), q["expect"], "only")
+
+
+def test_npe_on_remote_endpoint_fragment():
+    """Q1: merging a fragment without a remote endpoint into one whose remote endpoint
+    lacks a field throws (Endpoint.java:121-129 via Span.java:375-379). Parity unpinned."""
+    from zipkin_amd.model import Kind, span2
+    a = span2("a", None, "a", Kind.SERVER, "web", "client", False)
+    b = span2("a", None, "a", Kind.SERVER, "web", None, False)
+    with pytest.raises(O.ReferenceNPE):
+        O.DependencyLinker().put_trace([a, b])
