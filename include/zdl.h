@@ -1,0 +1,181 @@
+/*
+ * zdl.h — C ABI of the MI355X dependency-link engine (libzdl.so).
+ *
+ * This is the drop-in boundary for Zipkin's dependency-link hot path. The
+ * reference has no native code; each entry point below replaces one Java
+ * method of the path, and the JNI shim a maintainer would add calls exactly
+ * these functions. Paths are relative to
+ * /root/reference/zipkin/src/main/java/zipkin2/.
+ *
+ *   zdl_create / zdl_destroy  <- new DependencyLinker()          internal/DependencyLinker.java:42-48
+ *   zdl_put_spans             <- DependencyLinker.putTrace(List)  internal/DependencyLinker.java:53-151
+ *                                (one call = many putTrace calls: CSR-grouped traces)
+ *   zdl_link                  <- DependencyLinker.link()          internal/DependencyLinker.java:184-186,206-219
+ *   zdl_merge_links           <- DependencyLinker.merge(Iterable) internal/DependencyLinker.java:189-204
+ *   zdl_set_window            <- the QueryRequest.test time rule  storage/QueryRequest.java:262-279
+ *                                used by InMemoryStorage.getDependencies(endTs, lookback)
+ *                                storage/InMemoryStorage.java:323-348
+ *   status ZDL_EREF_NPE       <- the NullPointerException Span.Builder.merge throws
+ *                                (Span.java:375-379 -> Endpoint.java:121-129)
+ *
+ * Conventions: plain C, plain pointers and sizes. Return 0 (ZDL_OK) or a
+ * negative status; zdl_last_error() has the message. A context is used by one
+ * thread at a time (DependencyLinker is not thread-safe either); separate
+ * contexts may run concurrently. Every context owns one HIP stream on its
+ * device. Strings never cross this boundary: services, ipv4 and ipv6
+ * addresses are dictionary ids assigned by the caller, with optional rank
+ * tables giving each id's position in java.lang.String.compareTo order
+ * (needed because Trace.merge sorts endpoints by string, Trace.java:105-116).
+ */
+#ifndef ZDL_H
+#define ZDL_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ZDL_ABI_VERSION 1
+
+/* ---- status codes ---- */
+#define ZDL_OK          0
+#define ZDL_EINVAL     (-1)  /* bad argument (offsets not monotone, service id >= n_services, ...) */
+#define ZDL_ENOMEM     (-2)  /* device or host allocation failed */
+#define ZDL_EDEVICE    (-3)  /* HIP runtime error */
+#define ZDL_EREF_NPE   (-4)  /* the reference throws NullPointerException for this input (quirk Q1) */
+#define ZDL_EREF_IAE   (-5)  /* the reference throws IllegalArgumentException for this input */
+
+/* ---- port_flags column bit layout (one u32 per span) ---- */
+#define ZDL_PF_PORT_MASK     0x0000FFFFu /* local endpoint port, 0 = null (Endpoint.java:245-260) */
+#define ZDL_PF_KIND_SHIFT    16          /* 3 bits: Span.Kind ordinal, 7 = null */
+#define ZDL_KIND_CLIENT      0u
+#define ZDL_KIND_SERVER      1u
+#define ZDL_KIND_PRODUCER    2u
+#define ZDL_KIND_CONSUMER    3u
+#define ZDL_KIND_NULL        7u
+#define ZDL_PF_SHARED_SHIFT  19          /* 2 bits: 0 = shared null, 1 = false, 2 = true */
+#define ZDL_PF_ERROR         (1u << 21)  /* tags contain the key "error" */
+#define ZDL_PF_RIP4          (1u << 22)  /* remote endpoint carries an ipv4 */
+#define ZDL_PF_RIP6          (1u << 23)  /* remote endpoint carries an ipv6 */
+#define ZDL_PF_RPORT         (1u << 24)  /* remote endpoint carries a port */
+
+/* ---- dictionaries whose ranks can be set ---- */
+#define ZDL_DICT_SERVICE 0
+#define ZDL_DICT_IPV4    1
+#define ZDL_DICT_IPV6    2
+
+/* ---- output order for zdl_link ---- */
+#define ZDL_ORDER_SORTED      0  /* by (rank[parent], rank[child]) */
+#define ZDL_ORDER_FIRST_SEEN  1  /* only for zdl_merge_links output: DependencyLinker.merge order */
+
+/* ---- context flags ---- */
+#define ZDL_FLAG_TIMING  1u      /* record HIP events around every kernel (zdl_kernel_times) */
+
+/*
+ * Span columns, structure of arrays, n_spans entries each. A local endpoint is
+ * null iff local_svc, local_ip4, local_ip6 are -1 and the port is 0; a remote
+ * endpoint is null iff remote_svc is -1 and none of RIP4/RIP6/RPORT is set
+ * (Span.Builder coerces empty endpoints to null, Span.java:527-536).
+ */
+typedef struct zdl_span_cols {
+  const uint64_t* trace_lo;   /* low 64 bits of the trace id (sharding/grouping; not read by zdl_put_spans) */
+  const uint64_t* id;         /* span id, != 0 */
+  const uint64_t* parent_id;  /* 0 = null; parent_id == id is treated as null (Span.java:611-617) */
+  const int32_t*  local_svc;  /* service dictionary id, -1 = null */
+  const int32_t*  remote_svc; /* service dictionary id, -1 = null */
+  const int32_t*  local_ip4;  /* ipv4 dictionary id, -1 = null */
+  const int32_t*  local_ip6;  /* ipv6 dictionary id, -1 = null */
+  const uint32_t* port_flags; /* see ZDL_PF_* */
+  const int64_t*  timestamp;  /* epoch micros, 0 = absent; read only when a window is set */
+} zdl_span_cols;
+
+typedef struct zdl_config {
+  int32_t  device;      /* HIP device ordinal */
+  uint32_t n_services;  /* service dictionary size S; links are counted in an S x S table */
+  uint32_t flags;       /* ZDL_FLAG_* */
+  uint32_t reserved;
+} zdl_config;
+
+/* Links owned by the context; valid until the next zdl_link/zdl_merge_links/zdl_destroy. */
+typedef struct zdl_links {
+  uint64_t       n;
+  const int32_t* parent;       /* service dictionary ids */
+  const int32_t* child;
+  const int64_t* call_count;
+  const int64_t* error_count;
+} zdl_links;
+
+typedef struct zdl_kernel_times {
+  float plan_ms, tiles_ms, big_ms, reduce_ms, compact_ms;
+  uint32_t n_tiles, n_big, grid, reserved;
+} zdl_kernel_times;
+
+/* Context lifecycle. zdl_create returns NULL on failure (zdl_create_error() says why). */
+typedef struct zdl_ctx zdl_ctx;
+zdl_ctx*    zdl_create(const zdl_config* cfg);
+const char* zdl_create_error(void);
+void        zdl_destroy(zdl_ctx* ctx);
+const char* zdl_last_error(const zdl_ctx* ctx);
+int         zdl_abi_version(void);
+
+/* rank[id] = position of dictionary string `id` in java.lang.String order. Without a
+ * table the id itself is the rank. n must cover every id the columns use. */
+int zdl_set_ranks(zdl_ctx* ctx, int dict, const int32_t* rank, uint32_t n);
+
+/* Restrict subsequent puts to traces whose timestamp (QueryRequest.test rule) lies in
+ * [(end_ts_ms - lookback_ms) * 1000, end_ts_ms * 1000]; lookback_ms <= 0 clears it. */
+int zdl_set_window(zdl_ctx* ctx, int64_t end_ts_ms, int64_t lookback_ms);
+
+/* putTrace over n_traces CSR-grouped traces from HOST buffers: trace t is spans
+ * [trace_offsets[t], trace_offsets[t+1]) in storage order; trace_offsets has n_traces+1
+ * entries, starts at 0 and ends at n_spans. Synchronous. Counts accumulate in the
+ * context across calls. On ZDL_EREF_NPE the counts are unspecified until zdl_reset. */
+int zdl_put_spans(zdl_ctx* ctx, const zdl_span_cols* cols, uint64_t n_spans,
+                  const uint64_t* trace_offsets, uint64_t n_traces);
+
+/* Same, with every pointer (columns and offsets) in device memory of the context's
+ * device. Asynchronous on the context stream; errors surface at zdl_sync/zdl_link. */
+int zdl_put_spans_device(zdl_ctx* ctx, const zdl_span_cols* dev_cols, uint64_t n_spans,
+                         const uint64_t* dev_trace_offsets, uint64_t n_traces);
+
+/* Waits for the context stream and reports device-side status (e.g. ZDL_EREF_NPE). */
+int zdl_sync(zdl_ctx* ctx);
+
+/* DependencyLinker.link(): materialise the accumulated counts. The context keeps
+ * them (link() may be called again, like the reference). order: ZDL_ORDER_SORTED. */
+int zdl_link(zdl_ctx* ctx, int order, zdl_links* out);
+
+/* DependencyLinker.merge(links): sums call/error counts per (parent, child) of the n
+ * input links, on the device; output in first-seen order (ZDL_ORDER_FIRST_SEEN).
+ * Does not touch the context's accumulated counts. */
+int zdl_merge_links(zdl_ctx* ctx, const int32_t* parent, const int32_t* child,
+                    const int64_t* call_count, const int64_t* error_count, uint64_t n,
+                    zdl_links* out);
+
+/* Adds n pre-aggregated links to the context's accumulated counts (what
+ * DependencyLinker.merge does for stores that keep daily links, e.g.
+ * cassandra SelectDependencies.java:75-91); used when a context is re-created with a
+ * larger service dictionary. Synchronous. */
+int zdl_add_links(zdl_ctx* ctx, const int32_t* parent, const int32_t* child,
+                  const int64_t* call_count, const int64_t* error_count, uint64_t n);
+
+/* Clears the accumulated counts and the sticky device status. */
+int zdl_reset(zdl_ctx* ctx);
+
+/* Multi-GPU combine support: copy the S x S int64 call and error tables to/from device
+ * buffers of the same device (e.g. for an RCCL all-reduce), ordered on the ctx stream. */
+int zdl_table_export(zdl_ctx* ctx, void* dev_call, void* dev_err);
+int zdl_table_import(zdl_ctx* ctx, const void* dev_call, const void* dev_err);
+
+/* Kernel durations of the most recent put (+ link) when ZDL_FLAG_TIMING is set. */
+int zdl_get_kernel_times(zdl_ctx* ctx, zdl_kernel_times* out);
+
+/* The hipStream_t of the context, as an opaque pointer. */
+void* zdl_stream(zdl_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ZDL_H */

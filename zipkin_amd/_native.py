@@ -1,0 +1,212 @@
+"""ctypes binding of libzdl.so (include/zdl.h). The engine has no CPU fallback:
+if the library is missing or no device can be opened, calls raise."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libzdl.so")
+
+ZDL_OK, ZDL_EINVAL, ZDL_ENOMEM, ZDL_EDEVICE, ZDL_EREF_NPE, ZDL_EREF_IAE = 0, -1, -2, -3, -4, -5
+ZDL_DICT_SERVICE, ZDL_DICT_IPV4, ZDL_DICT_IPV6 = 0, 1, 2
+ZDL_ORDER_SORTED, ZDL_ORDER_FIRST_SEEN = 0, 1
+ZDL_FLAG_TIMING = 1
+
+PF_KIND_SHIFT = 16
+PF_SHARED_SHIFT = 19
+PF_ERROR = 1 << 21
+PF_RIP4 = 1 << 22
+PF_RIP6 = 1 << 23
+PF_RPORT = 1 << 24
+KIND_NULL = 7
+
+EXPORTS = (
+    "zdl_abi_version", "zdl_create", "zdl_create_error", "zdl_destroy", "zdl_last_error",
+    "zdl_set_ranks", "zdl_set_window", "zdl_put_spans", "zdl_put_spans_device", "zdl_sync",
+    "zdl_link", "zdl_merge_links", "zdl_add_links", "zdl_reset", "zdl_table_export",
+    "zdl_table_import", "zdl_get_kernel_times", "zdl_stream",
+)
+
+
+class SpanCols(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in (
+        "trace_lo", "id", "parent_id", "local_svc", "remote_svc", "local_ip4", "local_ip6",
+        "port_flags", "timestamp")]
+
+
+class Config(C.Structure):
+    _fields_ = [("device", C.c_int32), ("n_services", C.c_uint32), ("flags", C.c_uint32),
+                ("reserved", C.c_uint32)]
+
+
+class Links(C.Structure):
+    _fields_ = [("n", C.c_uint64), ("parent", C.POINTER(C.c_int32)), ("child", C.POINTER(C.c_int32)),
+                ("call_count", C.POINTER(C.c_int64)), ("error_count", C.POINTER(C.c_int64))]
+
+
+class KernelTimes(C.Structure):
+    _fields_ = [("plan_ms", C.c_float), ("tiles_ms", C.c_float), ("big_ms", C.c_float),
+                ("reduce_ms", C.c_float), ("compact_ms", C.c_float), ("n_tiles", C.c_uint32),
+                ("n_big", C.c_uint32), ("grid", C.c_uint32), ("reserved", C.c_uint32)]
+
+
+class ZdlError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"zdl error {code}: {msg}")
+        self.code = code
+
+
+class ReferenceNullPointerException(ZdlError):
+    """The reference throws java.lang.NullPointerException for this input (quirk Q1)."""
+
+
+class ReferenceIllegalArgumentException(ZdlError):
+    """The reference throws java.lang.IllegalArgumentException for this input."""
+
+
+_lib: Optional[C.CDLL] = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = C.CDLL(LIB_PATH)
+    vp, i32, u32, u64, i64 = C.c_void_p, C.c_int32, C.c_uint32, C.c_uint64, C.c_int64
+    L.zdl_abi_version.restype = C.c_int
+    L.zdl_create.restype = vp
+    L.zdl_create.argtypes = [C.POINTER(Config)]
+    L.zdl_create_error.restype = C.c_char_p
+    L.zdl_destroy.argtypes = [vp]
+    L.zdl_last_error.restype = C.c_char_p
+    L.zdl_last_error.argtypes = [vp]
+    L.zdl_set_ranks.argtypes = [vp, C.c_int, vp, u32]
+    L.zdl_set_window.argtypes = [vp, i64, i64]
+    L.zdl_put_spans.argtypes = [vp, C.POINTER(SpanCols), u64, vp, u64]
+    L.zdl_put_spans_device.argtypes = [vp, C.POINTER(SpanCols), u64, vp, u64]
+    L.zdl_sync.argtypes = [vp]
+    L.zdl_link.argtypes = [vp, C.c_int, C.POINTER(Links)]
+    L.zdl_merge_links.argtypes = [vp, vp, vp, vp, vp, u64, C.POINTER(Links)]
+    L.zdl_add_links.argtypes = [vp, vp, vp, vp, vp, u64]
+    L.zdl_reset.argtypes = [vp]
+    L.zdl_table_export.argtypes = [vp, vp, vp]
+    L.zdl_table_import.argtypes = [vp, vp, vp]
+    L.zdl_get_kernel_times.argtypes = [vp, C.POINTER(KernelTimes)]
+    L.zdl_stream.restype = vp
+    L.zdl_stream.argtypes = [vp]
+    for name in ("zdl_set_ranks", "zdl_set_window", "zdl_put_spans", "zdl_put_spans_device", "zdl_sync",
+                 "zdl_link", "zdl_merge_links", "zdl_add_links", "zdl_reset", "zdl_table_export",
+                 "zdl_table_import", "zdl_get_kernel_times"):
+        getattr(L, name).restype = C.c_int
+    _lib = L
+    return L
+
+
+def _ptr(a: Optional[np.ndarray]):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+class Context:
+    """One zdl_ctx: a device-resident link-count table for S services."""
+
+    def __init__(self, n_services: int, device: int = 0, timing: bool = False):
+        L = lib()
+        cfg = Config(device, int(n_services), ZDL_FLAG_TIMING if timing else 0, 0)
+        h = L.zdl_create(C.byref(cfg))
+        if not h:
+            raise ZdlError(ZDL_EDEVICE, L.zdl_create_error().decode())
+        self.h = C.c_void_p(h)
+        self.n_services = int(n_services)
+        self._L = L
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._L.zdl_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def check(self, rc: int):
+        if rc == ZDL_OK:
+            return
+        msg = self._L.zdl_last_error(self.h).decode()
+        if rc == ZDL_EREF_NPE:
+            raise ReferenceNullPointerException(rc, msg)
+        if rc == ZDL_EREF_IAE:
+            raise ReferenceIllegalArgumentException(rc, msg)
+        raise ZdlError(rc, msg)
+
+    def set_ranks(self, dict_id: int, ranks: np.ndarray):
+        r = np.ascontiguousarray(ranks, dtype=np.int32)
+        self.check(self._L.zdl_set_ranks(self.h, dict_id, _ptr(r), len(r)))
+
+    def set_window(self, end_ts_ms: int, lookback_ms: int):
+        self.check(self._L.zdl_set_window(self.h, int(end_ts_ms), int(lookback_ms)))
+
+    def put_spans(self, cols) -> None:
+        """cols: columnar.Columns (host numpy arrays)."""
+        sc = SpanCols(None, _ptr(cols.id), _ptr(cols.parent_id), _ptr(cols.local_svc), _ptr(cols.remote_svc),
+                      _ptr(cols.local_ip4), _ptr(cols.local_ip6), _ptr(cols.port_flags), _ptr(cols.timestamp))
+        self.check(self._L.zdl_put_spans(self.h, C.byref(sc), cols.n_spans, _ptr(cols.offsets), cols.n_traces))
+
+    def put_spans_device(self, ptrs: dict, n_spans: int, offsets_ptr: int, n_traces: int) -> None:
+        sc = SpanCols(None, *(ptrs.get(k) for k in ("id", "parent_id", "local_svc", "remote_svc", "local_ip4",
+                                                    "local_ip6", "port_flags", "timestamp")))
+        self.check(self._L.zdl_put_spans_device(self.h, C.byref(sc), n_spans, offsets_ptr, n_traces))
+
+    def sync(self):
+        self.check(self._L.zdl_sync(self.h))
+
+    @staticmethod
+    def _links_to_numpy(out: Links):
+        n = int(out.n)
+        if n == 0:
+            z32, z64 = np.zeros(0, np.int32), np.zeros(0, np.int64)
+            return z32, z32.copy(), z64, z64.copy()
+        return (np.ctypeslib.as_array(out.parent, (n,)).copy(), np.ctypeslib.as_array(out.child, (n,)).copy(),
+                np.ctypeslib.as_array(out.call_count, (n,)).copy(),
+                np.ctypeslib.as_array(out.error_count, (n,)).copy())
+
+    def link(self):
+        out = Links()
+        self.check(self._L.zdl_link(self.h, ZDL_ORDER_SORTED, C.byref(out)))
+        return self._links_to_numpy(out)
+
+    def merge_links(self, parent, child, call, err):
+        p, c = np.ascontiguousarray(parent, np.int32), np.ascontiguousarray(child, np.int32)
+        n, e = np.ascontiguousarray(call, np.int64), np.ascontiguousarray(err, np.int64)
+        out = Links()
+        self.check(self._L.zdl_merge_links(self.h, _ptr(p), _ptr(c), _ptr(n), _ptr(e), len(p), C.byref(out)))
+        return self._links_to_numpy(out)
+
+    def add_links(self, parent, child, call, err):
+        p, c = np.ascontiguousarray(parent, np.int32), np.ascontiguousarray(child, np.int32)
+        n, e = np.ascontiguousarray(call, np.int64), np.ascontiguousarray(err, np.int64)
+        self.check(self._L.zdl_add_links(self.h, _ptr(p), _ptr(c), _ptr(n), _ptr(e), len(p)))
+
+    def reset(self):
+        self.check(self._L.zdl_reset(self.h))
+
+    def table_export(self, dev_call: int, dev_err: int):
+        self.check(self._L.zdl_table_export(self.h, dev_call, dev_err))
+
+    def table_import(self, dev_call: int, dev_err: int):
+        self.check(self._L.zdl_table_import(self.h, dev_call, dev_err))
+
+    def kernel_times(self) -> KernelTimes:
+        t = KernelTimes()
+        self.check(self._L.zdl_get_kernel_times(self.h, C.byref(t)))
+        return t
+
+    def stream(self) -> int:
+        return self._L.zdl_stream(self.h) or 0

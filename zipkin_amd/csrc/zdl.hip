@@ -1,0 +1,1120 @@
+// zdl.hip — MI355X (gfx950) kernels and the C ABI of libzdl.so.
+//
+// Pipeline for one zdl_put_spans over CSR-grouped traces:
+//   k_plan    one pass over the trace offsets: tile -> first trace table, and the
+//             list of traces longer than SMALL_MAX ("big")
+//   k_tiles   persistent workgroups, each owns span tiles of TS spans: the traces
+//             that start in a tile are staged in LDS, sorted per trace, merged,
+//             turned into tree edges and linked; (parent, child) counts
+//             accumulate in an LDS table that is flushed once per workgroup
+//   k_big     one workgroup per big trace, same algorithm with HBM scratch and a
+//             bitonic sort
+//   k_reduce  sums the per-workgroup dense LDS tables into the S x S table
+// zdl_link compacts the non-zero cells (k_compact) and sorts them by service rank.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/zdl.h"
+#include "zdl_algo.h"
+
+namespace zdl {
+
+constexpr int TS = 512;            // span range per tile
+constexpr int SMALL_MAX = 128;     // longer traces go to k_big
+constexpr int CAP = TS + SMALL_MAX;  // LDS span slots per tile chunk
+constexpr int MAXT = 256;          // traces per chunk
+constexpr int WG = 512;            // threads per tile workgroup
+constexpr int BIG_WG = 1024;       // threads per big-trace workgroup
+constexpr int DENSE_MAX = 4096;    // S*S <= DENSE_MAX -> dense LDS counters
+constexpr int HCAP = 2048;         // LDS hash slots otherwise
+constexpr int HPROBE = 64;
+
+struct Cols {
+  const uint64_t* id;
+  const uint64_t* pid;
+  const int32_t* lsvc;
+  const int32_t* rsvc;
+  const int32_t* ip4;
+  const int32_t* ip6;
+  const uint32_t* pf;
+  const int64_t* ts;
+};
+
+struct Args {
+  Cols c;
+  const uint64_t* off;
+  uint64_t n_traces;
+  uint64_t n_spans;
+  const uint32_t* tile_first;
+  uint32_t n_tiles;
+  Ranks R;
+  uint32_t S;
+  int dense;
+  int window;
+  int64_t win_lo, win_hi;
+  unsigned long long* call;
+  unsigned long long* err;
+  uint32_t* slab;
+  const uint32_t* big_list;
+  const uint32_t* big_count;
+  uint32_t* status;
+  // big-trace scratch (HBM), indexed by global span index
+  uint64_t* b_id;
+  uint64_t* b_pid;
+  int32_t* b_lsvc;
+  int32_t* b_rsvc;
+  int32_t* b_ip4;
+  int32_t* b_ip6;
+  uint32_t* b_pf;
+  uint32_t* b_perm;
+  int32_t* b_parent;
+  uint8_t* b_live;
+  uint8_t* b_haschild;
+};
+
+// ------------------------------------------------------------------- k_plan
+__global__ void k_plan(const uint64_t* __restrict__ off, uint64_t n_traces, uint32_t n_tiles,
+                       uint32_t* __restrict__ tile_first, uint32_t* __restrict__ big_list,
+                       uint32_t* __restrict__ big_count, uint32_t* __restrict__ status) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t > n_traces) return;
+  const uint64_t o = off[t];
+  if (t < n_traces) {
+    const uint64_t e = off[t + 1];
+    if (e < o) { atomicOr(status, ST_BADOFF); return; }
+    if (e - o > (uint64_t)SMALL_MAX) big_list[atomicAdd(big_count, 1u)] = (uint32_t)t;
+  }
+  // tile_first[k] = min{t : off[t] >= k*TS}: trace t owns the k with k*TS in (off[t-1], off[t]]
+  const uint64_t lo = t == 0 ? 0 : off[t - 1] / TS + 1;
+  uint64_t hi = o / TS;
+  if (t == n_traces) hi = n_tiles;
+  if (hi > n_tiles) hi = n_tiles;
+  for (uint64_t k = lo; k <= hi; ++k) tile_first[k] = (uint32_t)t;
+}
+
+// ---------------------------------------------------- LDS accumulation table
+struct LdsTable {
+  uint32_t* a;  // dense: call[S*S], err[S*S]; hash: key[HCAP], call[HCAP], err[HCAP]
+  uint32_t S;
+  int dense;
+  unsigned long long* gcall;
+  unsigned long long* gerr;
+  uint32_t* status;
+
+  __device__ __forceinline__ void add(int32_t p, int32_t c, bool e) const {
+    if ((uint32_t)p >= S || (uint32_t)c >= S) { atomicOr(status, ST_BADSVC); return; }
+    const uint32_t idx = (uint32_t)p * S + (uint32_t)c;
+    if (dense) {
+      atomicAdd(&a[idx], 1u);
+      if (e) atomicAdd(&a[S * S + idx], 1u);
+      return;
+    }
+    const uint32_t key = idx + 1u;
+    uint32_t h = (key * 2654435761u) & (HCAP - 1);
+    for (int probe = 0; probe < HPROBE; ++probe) {
+      uint32_t k = a[h];
+      if (k == 0) {
+        k = atomicCAS(&a[h], 0u, key);
+        if (k == 0) k = key;
+      }
+      if (k == key) {
+        atomicAdd(&a[HCAP + h], 1u);
+        if (e) atomicAdd(&a[2 * HCAP + h], 1u);
+        return;
+      }
+      h = (h + 1) & (HCAP - 1);
+    }
+    atomicAdd(&gcall[idx], 1ull);  // LDS table full: straight to HBM
+    if (e) atomicAdd(&gerr[idx], 1ull);
+  }
+};
+
+// Block-wide exclusive scan of one u32 per thread (blockDim.x == WG).
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t* warp_sums, uint32_t& total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t incl = x;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += y;
+  }
+  if (lane == 63) warp_sums[w] = incl;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+    for (int i = 0; i < WG / 64; ++i) {
+      const uint32_t t = warp_sums[i];
+      warp_sums[i] = acc;
+      acc += t;
+    }
+    warp_sums[WG / 64] = acc;
+  }
+  __syncthreads();
+  const uint32_t r = warp_sums[w] + incl - x;
+  total = warp_sums[WG / 64];
+  __syncthreads();
+  return r;
+}
+
+// ------------------------------------------------------------------ k_tiles
+struct TileLds {
+  // byte offsets into the dynamic LDS block; every carve 16-B aligned
+  static constexpr size_t o_id = 0;
+  static constexpr size_t o_pid = o_id + 8 * CAP;
+  static constexpr size_t o_ts = o_pid + 8 * CAP;
+  static constexpr size_t o_lsvc = o_ts + 8 * CAP;
+  static constexpr size_t o_rsvc = o_lsvc + 4 * CAP;
+  static constexpr size_t o_ip4 = o_rsvc + 4 * CAP;
+  static constexpr size_t o_ip6 = o_ip4 + 4 * CAP;
+  static constexpr size_t o_pf = o_ip6 + 4 * CAP;
+  static constexpr size_t o_perm = o_pf + 4 * CAP;
+  static constexpr size_t o_seg = o_perm + 4 * CAP;
+  static constexpr size_t o_parent = o_seg + 4 * CAP;
+  static constexpr size_t o_live = o_parent + 4 * CAP;
+  static constexpr size_t o_hasc = o_live + CAP;
+  static constexpr size_t o_tloc = o_hasc + CAP;
+  static constexpr size_t o_tgoff = o_tloc + 4 * (MAXT + 4);
+  static constexpr size_t o_troot = o_tgoff + 8 * MAXT;
+  static constexpr size_t o_tact = o_troot + 4 * MAXT;
+  static constexpr size_t o_scan = o_tact + 4 * MAXT;
+  static constexpr size_t o_table = o_scan + 4 * 32;
+  static size_t bytes(uint32_t S, int dense) {
+    return o_table + (dense ? (size_t)8 * S * S : (size_t)12 * HCAP);
+  }
+};
+static_assert(TileLds::o_table % 16 == 0, "LDS carve alignment");
+
+__global__ void __launch_bounds__(WG, 2) k_tiles(Args A) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  View v;
+  v.id = (uint64_t*)(lds + TileLds::o_id);
+  v.pid = (uint64_t*)(lds + TileLds::o_pid);
+  v.lsvc = (int32_t*)(lds + TileLds::o_lsvc);
+  v.rsvc = (int32_t*)(lds + TileLds::o_rsvc);
+  v.ip4 = (int32_t*)(lds + TileLds::o_ip4);
+  v.ip6 = (int32_t*)(lds + TileLds::o_ip6);
+  v.pf = (uint32_t*)(lds + TileLds::o_pf);
+  v.perm = (uint32_t*)(lds + TileLds::o_perm);
+  v.parent = (int32_t*)(lds + TileLds::o_parent);
+  v.live = (uint8_t*)(lds + TileLds::o_live);
+  v.haschild = (uint8_t*)(lds + TileLds::o_hasc);
+  int64_t* s_ts = (int64_t*)(lds + TileLds::o_ts);
+  uint32_t* s_seg = (uint32_t*)(lds + TileLds::o_seg);
+  uint32_t* t_loc = (uint32_t*)(lds + TileLds::o_tloc);
+  uint64_t* t_goff = (uint64_t*)(lds + TileLds::o_tgoff);
+  int32_t* t_root = (int32_t*)(lds + TileLds::o_troot);
+  uint32_t* t_act = (uint32_t*)(lds + TileLds::o_tact);
+  uint32_t* scan = (uint32_t*)(lds + TileLds::o_scan);
+  uint32_t* table = (uint32_t*)(lds + TileLds::o_table);
+
+  const uint32_t tab_words = A.dense ? 2 * A.S * A.S : 3 * HCAP;
+  for (uint32_t i = threadIdx.x; i < tab_words; i += WG) table[i] = 0;
+  const LdsTable tab{table, A.S, A.dense, A.call, A.err, A.status};
+  bool npe = false;
+  __syncthreads();
+
+  for (uint32_t k = blockIdx.x; k < A.n_tiles; k += gridDim.x) {
+    const uint32_t tile_t0 = A.tile_first[k], tile_t1 = A.tile_first[k + 1];
+    for (uint32_t c0 = tile_t0; c0 < tile_t1; c0 += MAXT) {
+      const uint32_t nT = min((uint32_t)MAXT, tile_t1 - c0);
+      // ---- P0: trace extents -> local slot offsets
+      uint32_t len = 0;
+      if (threadIdx.x < nT) {
+        const uint64_t b = A.off[c0 + threadIdx.x], e = A.off[c0 + threadIdx.x + 1];
+        const uint64_t l = e - b;
+        len = l <= (uint64_t)SMALL_MAX ? (uint32_t)l : 0u;  // big traces: k_big
+        t_goff[threadIdx.x] = b;
+        t_root[threadIdx.x] = 0x7fffffff;
+        t_act[threadIdx.x] = 1;
+      }
+      uint32_t total;
+      const uint32_t loc = block_excl_scan(len, scan, total);
+      if (threadIdx.x < nT) t_loc[threadIdx.x] = loc;
+      if (threadIdx.x == 0) t_loc[nT] = total;
+      __syncthreads();
+      // ---- P1: stage the chunk's spans in LDS (coalesced within and across traces)
+      for (uint32_t s = threadIdx.x; s < total; s += WG) {
+        uint32_t lo = 0, hi = nT;  // last j with t_loc[j] <= s
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (t_loc[mid] <= s) lo = mid; else hi = mid;
+        }
+        const uint64_t g = t_goff[lo] + (s - t_loc[lo]);
+        s_seg[s] = lo;
+        const uint64_t id = A.c.id[g];
+        uint64_t pid = A.c.pid[g];
+        if (pid == id) pid = 0;  // Span.build drops a self parent (Span.java:611-617)
+        v.id[s] = id;
+        v.pid[s] = pid;
+        v.lsvc[s] = A.c.lsvc[g];
+        v.rsvc[s] = A.c.rsvc[g];
+        v.ip4[s] = A.c.ip4[g];
+        v.ip6[s] = A.c.ip6[g];
+        v.pf[s] = A.c.pf[g];
+        if (A.window) s_ts[s] = A.c.ts[g];
+      }
+      __syncthreads();
+      // ---- P2: time window per trace (QueryRequest.test), storage order
+      if (A.window) {
+        if (threadIdx.x < nT) {
+          int64_t ts = 0;
+          for (uint32_t s = t_loc[threadIdx.x]; s < t_loc[threadIdx.x + 1]; ++s) {
+            const int64_t x = s_ts[s];
+            if (x == 0) continue;
+            if (v.pid[s] == 0) { ts = x; break; }
+            if (ts == 0 || ts > x) ts = x;
+          }
+          t_act[threadIdx.x] = window_pass(ts, A.win_lo, A.win_hi) ? 1u : 0u;
+        }
+        __syncthreads();
+      }
+      // ---- P3: per-trace rank sort (Trace.merge's Collections.sort)
+      for (uint32_t s = threadIdx.x; s < total; s += WG) {
+        const uint32_t j = s_seg[s];
+        const uint32_t tb = t_loc[j], te = t_loc[j + 1];
+        uint32_t r = 0;
+        if (t_act[j]) {
+          const uint64_t my = v.id[s];
+          for (uint32_t q = tb; q < te; ++q) {
+            const uint64_t o = v.id[q];
+            if (o < my) ++r;
+            else if (o == my && q != s && span_less(v, A.R, q, s)) ++r;
+          }
+        } else {
+          r = s - tb;
+        }
+        v.perm[tb + r] = s;
+      }
+      __syncthreads();
+      // ---- P4: Trace.merge's greedy merge, one lane per id group
+      for (uint32_t p = threadIdx.x; p < total; p += WG) {
+        const uint32_t j = s_seg[p];
+        const uint32_t tb = t_loc[j], te = t_loc[j + 1];
+        v.haschild[p] = 0;
+        if (!t_act[j]) { v.live[p] = 0; continue; }
+        const uint64_t my = v.id[v.perm[p]];
+        if (p != tb && v.id[v.perm[p - 1]] == my) continue;
+        uint32_t ge = p + 1;
+        while (ge < te && v.id[v.perm[ge]] == my) ++ge;
+        if (ge == p + 1) { v.live[p] = 1; continue; }
+        npe |= merge_group(v, (int)p, (int)ge);
+      }
+      __syncthreads();
+      // ---- P5: the root = first non-shared cleaned span without a parent
+      for (uint32_t p = threadIdx.x; p < total; p += WG) {
+        const uint32_t s = v.perm[p];
+        if (v.live[p] && !is_shared(v.pf[s]) && v.pid[s] == 0) atomicMin(&t_root[s_seg[p]], (int32_t)p);
+      }
+      __syncthreads();
+      // ---- P6: tree edges, one lane per id group
+      for (uint32_t p = threadIdx.x; p < total; p += WG) {
+        const uint32_t j = s_seg[p];
+        if (!t_act[j]) { v.parent[p] = PAR_NONMEMBER; continue; }
+        const uint32_t tb = t_loc[j], te = t_loc[j + 1];
+        const uint64_t my = v.id[v.perm[p]];
+        if (p != tb && v.id[v.perm[p - 1]] == my) continue;
+        uint32_t ge = p + 1;
+        while (ge < te && v.id[v.perm[ge]] == my) ++ge;
+        const int32_t rp = t_root[j] == 0x7fffffff ? -1 : t_root[j];
+        resolve_group(v, (int)tb, (int)te, (int)p, (int)ge, rp);
+      }
+      __syncthreads();
+      // ---- P7: which nodes have children (CLIENT-with-children rule)
+      for (uint32_t p = threadIdx.x; p < total; p += WG) {
+        const int32_t q = v.parent[p];
+        if (q >= 0) v.haschild[q] = 1;
+      }
+      __syncthreads();
+      // ---- P8: breadth-first rules -> addLink into the LDS table
+      for (uint32_t p = threadIdx.x; p < total; p += WG) {
+        if (v.parent[p] == PAR_NONMEMBER) continue;
+        const uint32_t j = s_seg[p];
+        const int32_t rp = t_root[j] == 0x7fffffff ? -1 : t_root[j];
+        link_node(v, (int)p, rp, (int)(t_loc[j + 1] - t_loc[j]),
+                  [&](int32_t a, int32_t b, bool e) { tab.add(a, b, e); });
+      }
+      __syncthreads();
+    }
+  }
+  if (npe) atomicOr(A.status, ST_NPE);
+  // ---- flush: dense -> this workgroup's slab row; hash -> HBM atomics
+  if (A.dense) {
+    uint32_t* row = A.slab + (size_t)blockIdx.x * tab_words;
+    for (uint32_t i = threadIdx.x; i < tab_words; i += WG) row[i] = table[i];
+  } else {
+    for (uint32_t h = threadIdx.x; h < HCAP; h += WG) {
+      const uint32_t key = table[h];
+      if (key == 0) continue;
+      atomicAdd(&A.call[key - 1], (unsigned long long)table[HCAP + h]);
+      const uint32_t e = table[2 * HCAP + h];
+      if (e) atomicAdd(&A.err[key - 1], (unsigned long long)e);
+    }
+  }
+}
+
+// ----------------------------------------------------------------- k_reduce
+__global__ void k_reduce(const uint32_t* __restrict__ slab, uint32_t rows, uint32_t SS,
+                         unsigned long long* __restrict__ call, unsigned long long* __restrict__ err) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 2 * SS) return;
+  unsigned long long sum = 0;
+  for (uint32_t r = 0; r < rows; ++r) sum += slab[(size_t)r * 2 * SS + i];
+  if (sum == 0) return;
+  if (i < SS) call[i] += sum; else err[i - SS] += sum;
+}
+
+// -------------------------------------------------------------------- k_big
+// One workgroup per trace longer than SMALL_MAX; arrays live in HBM scratch at the
+// trace's global span offset. Same phases as k_tiles, bitonic sort instead of ranks.
+__device__ __forceinline__ void big_sync() { __syncthreads(); }
+
+__global__ void __launch_bounds__(BIG_WG) k_big(Args A) {
+  __shared__ int32_t sh_root;
+  __shared__ int sh_act;
+  __shared__ int64_t sh_ts_root_idx, sh_ts_min;
+  const uint32_t nbig = *A.big_count;
+  for (uint32_t bi = blockIdx.x; bi < nbig; bi += gridDim.x) {
+    const uint32_t t = A.big_list[bi];
+    const uint64_t b = A.off[t];
+    const int n = (int)(A.off[t + 1] - b);
+    View v;
+    v.id = A.b_id + b;
+    v.pid = A.b_pid + b;
+    v.lsvc = A.b_lsvc + b;
+    v.rsvc = A.b_rsvc + b;
+    v.ip4 = A.b_ip4 + b;
+    v.ip6 = A.b_ip6 + b;
+    v.pf = A.b_pf + b;
+    v.perm = A.b_perm + b;
+    v.parent = A.b_parent + b;
+    v.live = A.b_live + b;
+    v.haschild = A.b_haschild + b;
+    if (threadIdx.x == 0) {
+      sh_root = 0x7fffffff;
+      sh_act = 1;
+      sh_ts_root_idx = 0x7fffffffffffffffll;
+      sh_ts_min = 0;
+    }
+    for (int s = threadIdx.x; s < n; s += BIG_WG) {
+      const uint64_t g = b + s;
+      const uint64_t id = A.c.id[g];
+      uint64_t pid = A.c.pid[g];
+      if (pid == id) pid = 0;
+      v.id[s] = id;
+      v.pid[s] = pid;
+      v.lsvc[s] = A.c.lsvc[g];
+      v.rsvc[s] = A.c.rsvc[g];
+      v.ip4[s] = A.c.ip4[g];
+      v.ip6[s] = A.c.ip6[g];
+      v.pf[s] = A.c.pf[g];
+      v.perm[s] = s;
+      v.haschild[s] = 0;
+    }
+    big_sync();
+    if (A.window) {
+      // first parentless span with a timestamp (storage order), else the minimum one
+      for (int s = threadIdx.x; s < n; s += BIG_WG) {
+        const int64_t x = A.c.ts[b + s];
+        if (x == 0) continue;
+        if (v.pid[s] == 0) atomicMin((long long*)&sh_ts_root_idx, (long long)s);
+      }
+      big_sync();
+      if (threadIdx.x == 0 && sh_ts_root_idx != 0x7fffffffffffffffll)
+        sh_ts_min = A.c.ts[b + sh_ts_root_idx];
+      big_sync();
+      if (sh_ts_root_idx == 0x7fffffffffffffffll) {
+        for (int s = threadIdx.x; s < n; s += BIG_WG) {
+          const int64_t x = A.c.ts[b + s];
+          if (x != 0) {
+            // atomicMin over positive micros; 0 stays "unset"
+            unsigned long long* m = (unsigned long long*)&sh_ts_min;
+            unsigned long long cur = *m;
+            while ((cur == 0 || (unsigned long long)x < cur)) {
+              const unsigned long long prev = atomicCAS(m, cur, (unsigned long long)x);
+              if (prev == cur) break;
+              cur = prev;
+            }
+          }
+        }
+        big_sync();
+      }
+      if (threadIdx.x == 0) sh_act = window_pass(sh_ts_min, A.win_lo, A.win_hi) ? 1 : 0;
+      big_sync();
+      if (!sh_act) { big_sync(); continue; }
+    }
+    // bitonic sort of perm by span_less (any n: out-of-range partners are +inf)
+    int npad = 1;
+    while (npad < n) npad <<= 1;
+    for (int kk = 2; kk <= npad; kk <<= 1) {
+      for (int i = threadIdx.x; i < n; i += BIG_WG) {
+        const int l = i ^ (kk - 1);
+        if (l > i && l < n) {
+          const uint32_t a = v.perm[i], c = v.perm[l];
+          if (span_less(v, A.R, c, a)) { v.perm[i] = c; v.perm[l] = a; }
+        }
+      }
+      big_sync();
+      for (int jj = kk >> 2; jj > 0; jj >>= 1) {
+        for (int i = threadIdx.x; i < n; i += BIG_WG) {
+          const int l = i ^ jj;
+          if (l > i && l < n) {
+            const uint32_t a = v.perm[i], c = v.perm[l];
+            if (span_less(v, A.R, c, a)) { v.perm[i] = c; v.perm[l] = a; }
+          }
+        }
+        big_sync();
+      }
+    }
+    bool npe = false;
+    for (int p = threadIdx.x; p < n; p += BIG_WG) {
+      const uint64_t my = v.id[v.perm[p]];
+      if (p != 0 && v.id[v.perm[p - 1]] == my) continue;
+      int ge = p + 1;
+      while (ge < n && v.id[v.perm[ge]] == my) ++ge;
+      if (ge == p + 1) { v.live[p] = 1; continue; }
+      npe |= merge_group(v, p, ge);
+    }
+    if (npe) atomicOr(A.status, ST_NPE);
+    big_sync();
+    for (int p = threadIdx.x; p < n; p += BIG_WG) {
+      const uint32_t s = v.perm[p];
+      if (v.live[p] && !is_shared(v.pf[s]) && v.pid[s] == 0) atomicMin(&sh_root, p);
+    }
+    big_sync();
+    const int rp = sh_root == 0x7fffffff ? -1 : sh_root;
+    for (int p = threadIdx.x; p < n; p += BIG_WG) {
+      const uint64_t my = v.id[v.perm[p]];
+      if (p != 0 && v.id[v.perm[p - 1]] == my) continue;
+      int ge = p + 1;
+      while (ge < n && v.id[v.perm[ge]] == my) ++ge;
+      resolve_group(v, 0, n, p, ge, rp);
+    }
+    big_sync();
+    for (int p = threadIdx.x; p < n; p += BIG_WG) {
+      const int32_t q = v.parent[p];
+      if (q >= 0) v.haschild[q] = 1;
+    }
+    big_sync();
+    for (int p = threadIdx.x; p < n; p += BIG_WG) {
+      if (v.parent[p] == PAR_NONMEMBER) continue;
+      link_node(v, p, rp, n, [&](int32_t a, int32_t c, bool e) {
+        if ((uint32_t)a >= A.S || (uint32_t)c >= A.S) { atomicOr(A.status, ST_BADSVC); return; }
+        const size_t idx = (size_t)a * A.S + c;
+        atomicAdd(&A.call[idx], 1ull);
+        if (e) atomicAdd(&A.err[idx], 1ull);
+      });
+    }
+    big_sync();
+  }
+}
+
+// ---------------------------------------------------------------- k_compact
+__global__ void k_compact(const unsigned long long* __restrict__ call, const unsigned long long* __restrict__ err,
+                          uint64_t SS, uint32_t S, unsigned long long* __restrict__ count,
+                          int32_t* __restrict__ op, int32_t* __restrict__ oc, int64_t* __restrict__ ocall,
+                          int64_t* __restrict__ oerr) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= SS) return;
+  const unsigned long long n = call[i];
+  if (n == 0) return;
+  const unsigned long long w = atomicAdd(count, 1ull);
+  op[w] = (int32_t)(i / S);
+  oc[w] = (int32_t)(i % S);
+  ocall[w] = (int64_t)n;
+  oerr[w] = (int64_t)err[i];
+}
+
+// ---------------------------------------------------------- merge (DL.merge)
+// Sums input links per (parent, child) and records the first index each pair was seen
+// at, reproducing LinkedHashMap first-seen order (DependencyLinker.java:189-204).
+__global__ void k_merge_accum(const int32_t* __restrict__ p, const int32_t* __restrict__ c,
+                              const int64_t* __restrict__ call, const int64_t* __restrict__ err, uint64_t n,
+                              uint32_t S, unsigned long long* __restrict__ tcall,
+                              unsigned long long* __restrict__ terr, unsigned long long* __restrict__ tfirst,
+                              uint32_t* __restrict__ status) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if ((uint32_t)p[i] >= S || (uint32_t)c[i] >= S) { atomicOr(status, ST_BADSVC); return; }
+  const size_t idx = (size_t)p[i] * S + c[i];
+  atomicAdd(&tcall[idx], (unsigned long long)call[i]);
+  atomicAdd(&terr[idx], (unsigned long long)err[i]);
+  atomicMin(&tfirst[idx], (unsigned long long)i);
+}
+
+__global__ void k_merge_compact(const unsigned long long* __restrict__ tcall, const unsigned long long* __restrict__ terr,
+                                const unsigned long long* __restrict__ tfirst, uint64_t SS, uint32_t S,
+                                unsigned long long* __restrict__ count, int32_t* __restrict__ op,
+                                int32_t* __restrict__ oc, int64_t* __restrict__ ocall, int64_t* __restrict__ oerr,
+                                uint64_t* __restrict__ ofirst) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= SS) return;
+  if (tfirst[i] == ~0ull) return;
+  const unsigned long long w = atomicAdd(count, 1ull);
+  op[w] = (int32_t)(i / S);
+  oc[w] = (int32_t)(i % S);
+  ocall[w] = (int64_t)tcall[i];
+  oerr[w] = (int64_t)terr[i];
+  ofirst[w] = tfirst[i];
+}
+
+}  // namespace zdl
+
+// ====================================================================== host
+using namespace zdl;
+
+namespace {
+
+thread_local std::string g_create_error;
+
+template <class T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  hipError_t ensure(size_t want) {
+    if (want <= n) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    const size_t alloc = std::max<size_t>(want, 1);
+    hipError_t e = hipMalloc((void**)&p, alloc * sizeof(T));
+    if (e == hipSuccess) n = alloc;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+}  // namespace
+
+struct zdl_ctx {
+  int device = 0;
+  uint32_t S = 0;
+  uint32_t flags = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  int grid = 0;
+  // ranks
+  DevBuf<int32_t> rank[3];
+  uint32_t nrank[3] = {0, 0, 0};
+  // S x S counters
+  DevBuf<unsigned long long> call, errc;
+  DevBuf<uint32_t> status;
+  // per-put scratch
+  DevBuf<uint32_t> tile_first, big_list, big_count, slab;
+  DevBuf<uint64_t> b_id, b_pid;
+  DevBuf<int32_t> b_lsvc, b_rsvc, b_ip4, b_ip6, b_parent;
+  DevBuf<uint32_t> b_pf, b_perm;
+  DevBuf<uint8_t> b_live, b_hasc;
+  // host-API staging
+  DevBuf<uint64_t> h_id, h_pid, h_off;
+  DevBuf<int32_t> h_lsvc, h_rsvc, h_ip4, h_ip6;
+  DevBuf<uint32_t> h_pf;
+  DevBuf<int64_t> h_ts;
+  // link output
+  DevBuf<unsigned long long> count, m_call, m_err, m_first;
+  DevBuf<int32_t> o_p, o_c;
+  DevBuf<int64_t> o_call, o_err;
+  DevBuf<uint64_t> o_first;
+  DevBuf<int32_t> mi_p, mi_c;
+  DevBuf<int64_t> mi_call, mi_err;
+  std::vector<int32_t> out_p, out_c;
+  std::vector<int64_t> out_call, out_err;
+  std::vector<int32_t> host_rank[3];
+  // window
+  int window = 0;
+  int64_t win_lo = 0, win_hi = 0;
+  // timing
+  hipEvent_t ev[8] = {};
+  zdl_kernel_times times = {};
+};
+
+namespace {
+
+int fail(zdl_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+int hip_fail(zdl_ctx* c, hipError_t e, const char* what) {
+  return fail(c, e == hipErrorOutOfMemory ? ZDL_ENOMEM : ZDL_EDEVICE,
+              std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIP_TRY(c, expr)                                   \
+  do {                                                     \
+    hipError_t _e = (expr);                                \
+    if (_e != hipSuccess) return hip_fail((c), _e, #expr); \
+  } while (0)
+
+int status_code(zdl_ctx* c, uint32_t st) {
+  if (st & ST_NPE) return fail(c, ZDL_EREF_NPE, "reference throws NullPointerException (Span.Builder.merge of a null endpoint)");
+  if (st & ST_IAE) return fail(c, ZDL_EREF_IAE, "reference throws IllegalArgumentException");
+  if (st & ST_BADSVC) return fail(c, ZDL_EINVAL, "service id >= n_services");
+  if (st & ST_BADOFF) return fail(c, ZDL_EINVAL, "trace offsets are not non-decreasing");
+  return ZDL_OK;
+}
+
+void ev_record(zdl_ctx* c, int i) {
+  if (c->flags & ZDL_FLAG_TIMING) (void)hipEventRecord(c->ev[i], c->stream);
+}
+
+float ev_ms(zdl_ctx* c, int a, int b) {
+  float ms = 0.f;
+  if (hipEventElapsedTime(&ms, c->ev[a], c->ev[b]) != hipSuccess) return -1.f;
+  return ms;
+}
+
+}  // namespace
+
+extern "C" {
+
+int zdl_abi_version(void) { return ZDL_ABI_VERSION; }
+
+const char* zdl_create_error(void) { return g_create_error.c_str(); }
+
+zdl_ctx* zdl_create(const zdl_config* cfg) {
+  g_create_error.clear();
+  if (!cfg || cfg->n_services == 0 || cfg->n_services > 65535u) {
+    g_create_error = "n_services must be in [1, 65535]";
+    return nullptr;
+  }
+  zdl_ctx* c = new zdl_ctx();
+  c->device = cfg->device;
+  c->S = cfg->n_services;
+  c->flags = cfg->flags;
+  hipError_t e = hipSetDevice(c->device);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  const size_t SS = (size_t)c->S * c->S;
+  if (e == hipSuccess) e = c->call.ensure(SS);
+  if (e == hipSuccess) e = c->errc.ensure(SS);
+  if (e == hipSuccess) e = c->status.ensure(4);
+  if (e == hipSuccess) e = c->count.ensure(1);
+  if (e == hipSuccess) e = hipMemset(c->call.p, 0, SS * 8);
+  if (e == hipSuccess) e = hipMemset(c->errc.p, 0, SS * 8);
+  if (e == hipSuccess) e = hipMemset(c->status.p, 0, 16);
+  for (int i = 0; i < 8 && e == hipSuccess; ++i) e = hipEventCreate(&c->ev[i]);
+  if (e == hipSuccess) {
+    int cus = 0;
+    e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
+    c->grid = std::max(1, cus) * 2;  // two 512-thread workgroups per CU (LDS ~62-75 KB each)
+  }
+  if (e == hipSuccess) {
+    const int dense = SS <= (size_t)DENSE_MAX;
+    e = hipFuncSetAttribute((const void*)k_tiles, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)TileLds::bytes(c->S, dense));
+  }
+  if (e != hipSuccess) {
+    g_create_error = std::string("device init failed: ") + hipGetErrorString(e);
+    zdl_destroy(c);
+    return nullptr;
+  }
+  return c;
+}
+
+void zdl_destroy(zdl_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (auto& r : c->rank) r.release();
+  c->call.release(); c->errc.release(); c->status.release();
+  c->tile_first.release(); c->big_list.release(); c->big_count.release(); c->slab.release();
+  c->b_id.release(); c->b_pid.release(); c->b_lsvc.release(); c->b_rsvc.release(); c->b_ip4.release();
+  c->b_ip6.release(); c->b_parent.release(); c->b_pf.release(); c->b_perm.release(); c->b_live.release();
+  c->b_hasc.release();
+  c->h_id.release(); c->h_pid.release(); c->h_off.release(); c->h_lsvc.release(); c->h_rsvc.release();
+  c->h_ip4.release(); c->h_ip6.release(); c->h_pf.release(); c->h_ts.release();
+  c->count.release(); c->m_call.release(); c->m_err.release(); c->m_first.release();
+  c->o_p.release(); c->o_c.release(); c->o_call.release(); c->o_err.release(); c->o_first.release();
+  c->mi_p.release(); c->mi_c.release(); c->mi_call.release(); c->mi_err.release();
+  for (auto& ev : c->ev)
+    if (ev) (void)hipEventDestroy(ev);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char* zdl_last_error(const zdl_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+void* zdl_stream(zdl_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int zdl_set_ranks(zdl_ctx* c, int dict, const int32_t* rank, uint32_t n) {
+  if (!c || dict < 0 || dict > 2) return fail(c, ZDL_EINVAL, "bad dictionary");
+  HIP_TRY(c, hipSetDevice(c->device));
+  c->host_rank[dict].assign(rank, rank + n);
+  if (n == 0) {
+    c->nrank[dict] = 0;
+    return ZDL_OK;
+  }
+  HIP_TRY(c, c->rank[dict].ensure(n));
+  HIP_TRY(c, hipMemcpyAsync(c->rank[dict].p, rank, (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  c->nrank[dict] = n;
+  return ZDL_OK;
+}
+
+int zdl_set_window(zdl_ctx* c, int64_t end_ts_ms, int64_t lookback_ms) {
+  if (!c) return ZDL_EINVAL;
+  if (lookback_ms <= 0) {
+    c->window = 0;
+    return ZDL_OK;
+  }
+  c->window = 1;
+  c->win_hi = end_ts_ms * 1000;
+  c->win_lo = (end_ts_ms - lookback_ms) * 1000;
+  return ZDL_OK;
+}
+
+int zdl_put_spans_device(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans, const uint64_t* off,
+                         uint64_t n_traces) {
+  if (!c || !col) return fail(c, ZDL_EINVAL, "null argument");
+  if (n_traces == 0 || n_spans == 0) return ZDL_OK;
+  if (!col->id || !col->parent_id || !col->local_svc || !col->remote_svc || !col->local_ip4 ||
+      !col->local_ip6 || !col->port_flags || !off)
+    return fail(c, ZDL_EINVAL, "missing column");
+  if (c->window && !col->timestamp) return fail(c, ZDL_EINVAL, "window set but no timestamp column");
+  if (n_traces >= 0xffffffffull || n_spans >= (1ull << 40)) return fail(c, ZDL_EINVAL, "input too large");
+  HIP_TRY(c, hipSetDevice(c->device));
+  const uint32_t n_tiles = (uint32_t)((n_spans + TS - 1) / TS);
+  const size_t SS = (size_t)c->S * c->S;
+  const int dense = SS <= (size_t)DENSE_MAX;
+  const int grid = (int)std::min<uint32_t>((uint32_t)c->grid, std::max<uint32_t>(n_tiles, 1));
+  HIP_TRY(c, c->tile_first.ensure((size_t)n_tiles + 1));
+  HIP_TRY(c, c->big_list.ensure(n_traces));
+  HIP_TRY(c, c->big_count.ensure(1));
+  if (dense) HIP_TRY(c, c->slab.ensure((size_t)grid * 2 * SS));
+
+  Args A{};
+  A.c = Cols{col->id, col->parent_id, col->local_svc, col->remote_svc, col->local_ip4, col->local_ip6,
+             col->port_flags, col->timestamp};
+  A.off = off;
+  A.n_traces = n_traces;
+  A.n_spans = n_spans;
+  A.tile_first = c->tile_first.p;
+  A.n_tiles = n_tiles;
+  A.R = Ranks{c->nrank[0] ? c->rank[0].p : nullptr, c->nrank[1] ? c->rank[1].p : nullptr,
+              c->nrank[2] ? c->rank[2].p : nullptr, c->nrank[0], c->nrank[1], c->nrank[2]};
+  A.S = c->S;
+  A.dense = dense;
+  A.window = c->window;
+  A.win_lo = c->win_lo;
+  A.win_hi = c->win_hi;
+  A.call = c->call.p;
+  A.err = c->errc.p;
+  A.slab = c->slab.p;
+  A.big_list = c->big_list.p;
+  A.big_count = c->big_count.p;
+  A.status = c->status.p;
+
+  ev_record(c, 0);
+  HIP_TRY(c, hipMemsetAsync(c->big_count.p, 0, 4, c->stream));
+  {
+    const uint64_t threads = n_traces + 1;
+    hipLaunchKernelGGL(k_plan, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, c->stream, off, n_traces,
+                       n_tiles, c->tile_first.p, c->big_list.p, c->big_count.p, c->status.p);
+    HIP_TRY(c, hipGetLastError());
+  }
+  ev_record(c, 1);
+  hipLaunchKernelGGL(k_tiles, dim3(grid), dim3(WG), TileLds::bytes(c->S, dense), c->stream, A);
+  HIP_TRY(c, hipGetLastError());
+  ev_record(c, 2);
+  if (dense) {
+    hipLaunchKernelGGL(k_reduce, dim3((unsigned)((2 * SS + 255) / 256)), dim3(256), 0, c->stream, c->slab.p,
+                       (uint32_t)grid, (uint32_t)SS, c->call.p, c->errc.p);
+    HIP_TRY(c, hipGetLastError());
+  }
+  ev_record(c, 3);
+  // big traces: scratch sized by the whole input (only big-trace spans are touched)
+  HIP_TRY(c, c->b_id.ensure(n_spans));
+  HIP_TRY(c, c->b_pid.ensure(n_spans));
+  HIP_TRY(c, c->b_lsvc.ensure(n_spans));
+  HIP_TRY(c, c->b_rsvc.ensure(n_spans));
+  HIP_TRY(c, c->b_ip4.ensure(n_spans));
+  HIP_TRY(c, c->b_ip6.ensure(n_spans));
+  HIP_TRY(c, c->b_pf.ensure(n_spans));
+  HIP_TRY(c, c->b_perm.ensure(n_spans));
+  HIP_TRY(c, c->b_parent.ensure(n_spans));
+  HIP_TRY(c, c->b_live.ensure(n_spans));
+  HIP_TRY(c, c->b_hasc.ensure(n_spans));
+  A.b_id = c->b_id.p;
+  A.b_pid = c->b_pid.p;
+  A.b_lsvc = c->b_lsvc.p;
+  A.b_rsvc = c->b_rsvc.p;
+  A.b_ip4 = c->b_ip4.p;
+  A.b_ip6 = c->b_ip6.p;
+  A.b_pf = c->b_pf.p;
+  A.b_perm = c->b_perm.p;
+  A.b_parent = c->b_parent.p;
+  A.b_live = c->b_live.p;
+  A.b_haschild = c->b_hasc.p;
+  hipLaunchKernelGGL(k_big, dim3(256), dim3(BIG_WG), 0, c->stream, A);
+  HIP_TRY(c, hipGetLastError());
+  ev_record(c, 4);
+  c->times.n_tiles = n_tiles;
+  c->times.grid = (uint32_t)grid;
+  return ZDL_OK;
+}
+
+int zdl_sync(zdl_ctx* c) {
+  if (!c) return ZDL_EINVAL;
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  uint32_t st = 0;
+  HIP_TRY(c, hipMemcpy(&st, c->status.p, 4, hipMemcpyDeviceToHost));
+  if (c->flags & ZDL_FLAG_TIMING) {
+    c->times.plan_ms = ev_ms(c, 0, 1);
+    c->times.tiles_ms = ev_ms(c, 1, 2);
+    c->times.reduce_ms = ev_ms(c, 2, 3);
+    c->times.big_ms = ev_ms(c, 3, 4);
+  }
+  return status_code(c, st);
+}
+
+int zdl_put_spans(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans, const uint64_t* off,
+                  uint64_t n_traces) {
+  if (!c || !col || (!off && n_traces)) return fail(c, ZDL_EINVAL, "null argument");
+  if (n_traces == 0) return ZDL_OK;
+  if (off[0] != 0 || off[n_traces] != n_spans) return fail(c, ZDL_EINVAL, "trace offsets must span [0, n_spans]");
+  for (uint64_t t = 0; t < n_traces; ++t)
+    if (off[t + 1] < off[t]) return fail(c, ZDL_EINVAL, "trace offsets are not non-decreasing");
+  if (n_spans == 0) return ZDL_OK;
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, c->h_id.ensure(n_spans));
+  HIP_TRY(c, c->h_pid.ensure(n_spans));
+  HIP_TRY(c, c->h_lsvc.ensure(n_spans));
+  HIP_TRY(c, c->h_rsvc.ensure(n_spans));
+  HIP_TRY(c, c->h_ip4.ensure(n_spans));
+  HIP_TRY(c, c->h_ip6.ensure(n_spans));
+  HIP_TRY(c, c->h_pf.ensure(n_spans));
+  HIP_TRY(c, c->h_off.ensure(n_traces + 1));
+  hipStream_t s = c->stream;
+  HIP_TRY(c, hipMemcpyAsync(c->h_id.p, col->id, n_spans * 8, hipMemcpyHostToDevice, s));
+  HIP_TRY(c, hipMemcpyAsync(c->h_pid.p, col->parent_id, n_spans * 8, hipMemcpyHostToDevice, s));
+  HIP_TRY(c, hipMemcpyAsync(c->h_lsvc.p, col->local_svc, n_spans * 4, hipMemcpyHostToDevice, s));
+  HIP_TRY(c, hipMemcpyAsync(c->h_rsvc.p, col->remote_svc, n_spans * 4, hipMemcpyHostToDevice, s));
+  HIP_TRY(c, hipMemcpyAsync(c->h_ip4.p, col->local_ip4, n_spans * 4, hipMemcpyHostToDevice, s));
+  HIP_TRY(c, hipMemcpyAsync(c->h_ip6.p, col->local_ip6, n_spans * 4, hipMemcpyHostToDevice, s));
+  HIP_TRY(c, hipMemcpyAsync(c->h_pf.p, col->port_flags, n_spans * 4, hipMemcpyHostToDevice, s));
+  HIP_TRY(c, hipMemcpyAsync(c->h_off.p, off, (n_traces + 1) * 8, hipMemcpyHostToDevice, s));
+  zdl_span_cols d{};
+  d.trace_lo = nullptr;
+  d.id = c->h_id.p;
+  d.parent_id = c->h_pid.p;
+  d.local_svc = c->h_lsvc.p;
+  d.remote_svc = c->h_rsvc.p;
+  d.local_ip4 = c->h_ip4.p;
+  d.local_ip6 = c->h_ip6.p;
+  d.port_flags = c->h_pf.p;
+  if (c->window) {
+    if (!col->timestamp) return fail(c, ZDL_EINVAL, "window set but no timestamp column");
+    HIP_TRY(c, c->h_ts.ensure(n_spans));
+    HIP_TRY(c, hipMemcpyAsync(c->h_ts.p, col->timestamp, n_spans * 8, hipMemcpyHostToDevice, s));
+    d.timestamp = c->h_ts.p;
+  }
+  int rc = zdl_put_spans_device(c, &d, n_spans, c->h_off.p, n_traces);
+  if (rc != ZDL_OK) return rc;
+  return zdl_sync(c);
+}
+
+int zdl_reset(zdl_ctx* c) {
+  if (!c) return ZDL_EINVAL;
+  HIP_TRY(c, hipSetDevice(c->device));
+  const size_t SS = (size_t)c->S * c->S;
+  HIP_TRY(c, hipMemsetAsync(c->call.p, 0, SS * 8, c->stream));
+  HIP_TRY(c, hipMemsetAsync(c->errc.p, 0, SS * 8, c->stream));
+  HIP_TRY(c, hipMemsetAsync(c->status.p, 0, 16, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return ZDL_OK;
+}
+
+static void sort_output(zdl_ctx* c, size_t n) {
+  const std::vector<int32_t>& r = c->host_rank[0];
+  auto rk = [&](int32_t id) -> int64_t { return (size_t)id < r.size() ? r[id] : id; };
+  std::vector<uint32_t> idx(n);
+  for (size_t i = 0; i < n; ++i) idx[i] = (uint32_t)i;
+  std::sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) {
+    const int64_t pa = rk(c->out_p[a]), pb = rk(c->out_p[b]);
+    if (pa != pb) return pa < pb;
+    return rk(c->out_c[a]) < rk(c->out_c[b]);
+  });
+  std::vector<int32_t> p(n), ch(n);
+  std::vector<int64_t> ca(n), er(n);
+  for (size_t i = 0; i < n; ++i) {
+    p[i] = c->out_p[idx[i]];
+    ch[i] = c->out_c[idx[i]];
+    ca[i] = c->out_call[idx[i]];
+    er[i] = c->out_err[idx[i]];
+  }
+  c->out_p.swap(p);
+  c->out_c.swap(ch);
+  c->out_call.swap(ca);
+  c->out_err.swap(er);
+}
+
+int zdl_link(zdl_ctx* c, int order, zdl_links* out) {
+  if (!c || !out) return ZDL_EINVAL;
+  if (order != ZDL_ORDER_SORTED) return fail(c, ZDL_EINVAL, "zdl_link supports ZDL_ORDER_SORTED");
+  HIP_TRY(c, hipSetDevice(c->device));
+  const uint64_t SS = (uint64_t)c->S * c->S;
+  HIP_TRY(c, c->o_p.ensure(SS));
+  HIP_TRY(c, c->o_c.ensure(SS));
+  HIP_TRY(c, c->o_call.ensure(SS));
+  HIP_TRY(c, c->o_err.ensure(SS));
+  ev_record(c, 5);
+  HIP_TRY(c, hipMemsetAsync(c->count.p, 0, 8, c->stream));
+  hipLaunchKernelGGL(k_compact, dim3((unsigned)((SS + 255) / 256)), dim3(256), 0, c->stream, c->call.p, c->errc.p,
+                     SS, c->S, c->count.p, c->o_p.p, c->o_c.p, c->o_call.p, c->o_err.p);
+  HIP_TRY(c, hipGetLastError());
+  ev_record(c, 6);
+  unsigned long long n = 0;
+  HIP_TRY(c, hipMemcpyAsync(&n, c->count.p, 8, hipMemcpyDeviceToHost, c->stream));
+  int rc = zdl_sync(c);
+  if (rc != ZDL_OK) return rc;
+  if (c->flags & ZDL_FLAG_TIMING) c->times.compact_ms = ev_ms(c, 5, 6);
+  c->out_p.resize(n);
+  c->out_c.resize(n);
+  c->out_call.resize(n);
+  c->out_err.resize(n);
+  if (n) {
+    HIP_TRY(c, hipMemcpyAsync(c->out_p.data(), c->o_p.p, n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(c->out_c.data(), c->o_c.p, n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(c->out_call.data(), c->o_call.p, n * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(c->out_err.data(), c->o_err.p, n * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+  }
+  sort_output(c, n);
+  out->n = n;
+  out->parent = c->out_p.data();
+  out->child = c->out_c.data();
+  out->call_count = c->out_call.data();
+  out->error_count = c->out_err.data();
+  return ZDL_OK;
+}
+
+int zdl_merge_links(zdl_ctx* c, const int32_t* parent, const int32_t* child, const int64_t* call_count,
+                    const int64_t* error_count, uint64_t n, zdl_links* out) {
+  if (!c || !out) return ZDL_EINVAL;
+  HIP_TRY(c, hipSetDevice(c->device));
+  const uint64_t SS = (uint64_t)c->S * c->S;
+  HIP_TRY(c, c->m_call.ensure(SS));
+  HIP_TRY(c, c->m_err.ensure(SS));
+  HIP_TRY(c, c->m_first.ensure(SS));
+  HIP_TRY(c, c->o_p.ensure(SS));
+  HIP_TRY(c, c->o_c.ensure(SS));
+  HIP_TRY(c, c->o_call.ensure(SS));
+  HIP_TRY(c, c->o_err.ensure(SS));
+  HIP_TRY(c, c->o_first.ensure(SS));
+  HIP_TRY(c, c->mi_p.ensure(n));
+  HIP_TRY(c, c->mi_c.ensure(n));
+  HIP_TRY(c, c->mi_call.ensure(n));
+  HIP_TRY(c, c->mi_err.ensure(n));
+  hipStream_t s = c->stream;
+  HIP_TRY(c, hipMemsetAsync(c->m_call.p, 0, SS * 8, s));
+  HIP_TRY(c, hipMemsetAsync(c->m_err.p, 0, SS * 8, s));
+  HIP_TRY(c, hipMemsetAsync(c->m_first.p, 0xff, SS * 8, s));
+  HIP_TRY(c, hipMemsetAsync(c->count.p, 0, 8, s));
+  HIP_TRY(c, hipMemsetAsync(c->status.p, 0, 16, s));
+  if (n) {
+    HIP_TRY(c, hipMemcpyAsync(c->mi_p.p, parent, n * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(c, hipMemcpyAsync(c->mi_c.p, child, n * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(c, hipMemcpyAsync(c->mi_call.p, call_count, n * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(c, hipMemcpyAsync(c->mi_err.p, error_count, n * 8, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_merge_accum, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, c->mi_p.p, c->mi_c.p,
+                       c->mi_call.p, c->mi_err.p, n, c->S, c->m_call.p, c->m_err.p, c->m_first.p, c->status.p);
+    HIP_TRY(c, hipGetLastError());
+  }
+  hipLaunchKernelGGL(k_merge_compact, dim3((unsigned)((SS + 255) / 256)), dim3(256), 0, s, c->m_call.p, c->m_err.p,
+                     c->m_first.p, SS, c->S, c->count.p, c->o_p.p, c->o_c.p, c->o_call.p, c->o_err.p, c->o_first.p);
+  HIP_TRY(c, hipGetLastError());
+  unsigned long long m = 0;
+  HIP_TRY(c, hipMemcpyAsync(&m, c->count.p, 8, hipMemcpyDeviceToHost, s));
+  int rc = zdl_sync(c);
+  if (rc != ZDL_OK) return rc;
+  std::vector<uint64_t> first(m);
+  c->out_p.resize(m);
+  c->out_c.resize(m);
+  c->out_call.resize(m);
+  c->out_err.resize(m);
+  if (m) {
+    HIP_TRY(c, hipMemcpy(c->out_p.data(), c->o_p.p, m * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(c, hipMemcpy(c->out_c.data(), c->o_c.p, m * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(c, hipMemcpy(c->out_call.data(), c->o_call.p, m * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(c, hipMemcpy(c->out_err.data(), c->o_err.p, m * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(c, hipMemcpy(first.data(), c->o_first.p, m * 8, hipMemcpyDeviceToHost));
+  }
+  std::vector<uint32_t> idx(m);
+  for (size_t i = 0; i < m; ++i) idx[i] = (uint32_t)i;
+  std::sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) { return first[a] < first[b]; });
+  std::vector<int32_t> p(m), ch(m);
+  std::vector<int64_t> ca(m), er(m);
+  for (size_t i = 0; i < m; ++i) {
+    p[i] = c->out_p[idx[i]];
+    ch[i] = c->out_c[idx[i]];
+    ca[i] = c->out_call[idx[i]];
+    er[i] = c->out_err[idx[i]];
+  }
+  c->out_p.swap(p);
+  c->out_c.swap(ch);
+  c->out_call.swap(ca);
+  c->out_err.swap(er);
+  out->n = m;
+  out->parent = c->out_p.data();
+  out->child = c->out_c.data();
+  out->call_count = c->out_call.data();
+  out->error_count = c->out_err.data();
+  return ZDL_OK;
+}
+
+int zdl_add_links(zdl_ctx* c, const int32_t* parent, const int32_t* child, const int64_t* call_count,
+                  const int64_t* error_count, uint64_t n) {
+  if (!c) return ZDL_EINVAL;
+  if (n == 0) return ZDL_OK;
+  HIP_TRY(c, hipSetDevice(c->device));
+  const uint64_t SS = (uint64_t)c->S * c->S;
+  HIP_TRY(c, c->m_first.ensure(SS));
+  HIP_TRY(c, c->mi_p.ensure(n));
+  HIP_TRY(c, c->mi_c.ensure(n));
+  HIP_TRY(c, c->mi_call.ensure(n));
+  HIP_TRY(c, c->mi_err.ensure(n));
+  hipStream_t s = c->stream;
+  HIP_TRY(c, hipMemcpyAsync(c->mi_p.p, parent, n * 4, hipMemcpyHostToDevice, s));
+  HIP_TRY(c, hipMemcpyAsync(c->mi_c.p, child, n * 4, hipMemcpyHostToDevice, s));
+  HIP_TRY(c, hipMemcpyAsync(c->mi_call.p, call_count, n * 8, hipMemcpyHostToDevice, s));
+  HIP_TRY(c, hipMemcpyAsync(c->mi_err.p, error_count, n * 8, hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_merge_accum, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, c->mi_p.p, c->mi_c.p,
+                     c->mi_call.p, c->mi_err.p, n, c->S, c->call.p, c->errc.p, c->m_first.p, c->status.p);
+  HIP_TRY(c, hipGetLastError());
+  return zdl_sync(c);
+}
+
+int zdl_table_export(zdl_ctx* c, void* dev_call, void* dev_err) {
+  if (!c || !dev_call || !dev_err) return ZDL_EINVAL;
+  HIP_TRY(c, hipSetDevice(c->device));
+  const size_t bytes = (size_t)c->S * c->S * 8;
+  HIP_TRY(c, hipMemcpyAsync(dev_call, c->call.p, bytes, hipMemcpyDeviceToDevice, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(dev_err, c->errc.p, bytes, hipMemcpyDeviceToDevice, c->stream));
+  return ZDL_OK;
+}
+
+int zdl_table_import(zdl_ctx* c, const void* dev_call, const void* dev_err) {
+  if (!c || !dev_call || !dev_err) return ZDL_EINVAL;
+  HIP_TRY(c, hipSetDevice(c->device));
+  const size_t bytes = (size_t)c->S * c->S * 8;
+  HIP_TRY(c, hipMemcpyAsync(c->call.p, dev_call, bytes, hipMemcpyDeviceToDevice, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(c->errc.p, dev_err, bytes, hipMemcpyDeviceToDevice, c->stream));
+  return ZDL_OK;
+}
+
+int zdl_get_kernel_times(zdl_ctx* c, zdl_kernel_times* out) {
+  if (!c || !out) return ZDL_EINVAL;
+  *out = c->times;
+  return ZDL_OK;
+}
+
+}  // extern "C"

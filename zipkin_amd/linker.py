@@ -1,0 +1,123 @@
+"""DependencyLinker on the MI355X engine.
+
+Same surface as zipkin2.internal.DependencyLinker
+(zipkin/src/main/java/zipkin2/internal/DependencyLinker.java:37-247):
+``putTrace(spans)`` (one trace per call, returns self; empty list is a no-op),
+``link()`` (a new list every call; the linker stays usable) and the static
+``merge(links)``. Not thread-safe, like the reference. Where the reference
+throws, this raises: ReferenceNullPointerException for quirk Q1
+(Span.Builder.merge of a null endpoint), ReferenceIllegalArgumentException.
+
+Work runs in libzdl (include/zdl.h) on the GPU; there is no CPU path.
+Output order: the reference returns links in LinkedHashMap insertion order;
+this returns them sorted by (parent, child) in String order.
+``merge`` keeps the reference's first-seen order.
+"""
+from __future__ import annotations
+
+from typing import Iterable, List, Optional, Sequence
+
+import numpy as np
+
+from . import _native as N
+from .columnar import Columns, Dictionary, pack_traces
+from .model import DependencyLink, Span
+
+MIN_SERVICES = 64  # S*S <= 4096 keeps the engine on its dense LDS counters
+
+
+def _capacity(n: int) -> int:
+    cap = MIN_SERVICES
+    while cap < n:
+        cap *= 2
+    return cap
+
+
+class DependencyLinker:
+    def __init__(self, device: int = 0):
+        self.device = device
+        self.svc = Dictionary()
+        self.ip4 = Dictionary()
+        self.ip6 = Dictionary()
+        self._ctx: Optional[N.Context] = None
+        self._ranked = (-1, -1, -1)
+
+    # -- context management -------------------------------------------------
+    def _context(self) -> N.Context:
+        need = _capacity(max(len(self.svc), 1))
+        if self._ctx is None:
+            self._ctx = N.Context(need, self.device)
+            self._ranked = (-1, -1, -1)
+        elif self._ctx.n_services < need:
+            # grow the S x S table: carry the counts over on the device
+            p, c, n, e = self._ctx.link()
+            old = self._ctx
+            self._ctx = N.Context(need, self.device)
+            self._ranked = (-1, -1, -1)
+            if len(p):
+                self._ctx.add_links(p, c, n, e)
+            old.close()
+        sizes = (len(self.svc), len(self.ip4), len(self.ip6))
+        if sizes != self._ranked:
+            self._ctx.set_ranks(N.ZDL_DICT_SERVICE, self.svc.ranks())
+            self._ctx.set_ranks(N.ZDL_DICT_IPV4, self.ip4.ranks())
+            self._ctx.set_ranks(N.ZDL_DICT_IPV6, self.ip6.ranks())
+            self._ranked = sizes
+        return self._ctx
+
+    # -- reference API --------------------------------------------------------
+    def put_trace(self, spans: Sequence[Span]) -> "DependencyLinker":
+        """putTrace (DependencyLinker.java:53): spans of one trace."""
+        if not spans:
+            return self
+        return self.put_traces([spans])
+
+    def put_traces(self, traces: Sequence[Sequence[Span]]) -> "DependencyLinker":
+        """Batch of putTrace calls in one engine launch."""
+        traces = [t for t in traces if t]
+        if not traces:
+            return self
+        cols = pack_traces(traces, self.svc, self.ip4, self.ip6)
+        self.put_columns(cols)
+        return self
+
+    def put_columns(self, cols: Columns) -> "DependencyLinker":
+        """Already-packed traces (dictionary ids must come from this linker's dictionaries)."""
+        ctx = self._context()
+        ctx.put_spans(cols)
+        return self
+
+    def link(self) -> List[DependencyLink]:
+        """link() (DependencyLinker.java:184)."""
+        if self._ctx is None:
+            return []
+        p, c, n, e = self._ctx.link()
+        s = self.svc.strings
+        return [DependencyLink.create(s[a], s[b], int(x), int(y)) for a, b, x, y in zip(p, c, n, e)]
+
+    @staticmethod
+    def merge(links: Iterable[DependencyLink], device: int = 0) -> List[DependencyLink]:
+        """merge(Iterable) (DependencyLinker.java:189-204), first-seen order, on the device."""
+        links = list(links)
+        if not links:
+            return []
+        d = Dictionary()
+        p = np.array([d.id(l.parent) for l in links], np.int32)
+        c = np.array([d.id(l.child) for l in links], np.int32)
+        n = np.array([l.call_count for l in links], np.int64)
+        e = np.array([l.error_count for l in links], np.int64)
+        ctx = N.Context(_capacity(len(d)), device)
+        try:
+            mp, mc, mn, me = ctx.merge_links(p, c, n, e)
+        finally:
+            ctx.close()
+        return [DependencyLink.create(d.strings[a], d.strings[b], int(x), int(y))
+                for a, b, x, y in zip(mp, mc, mn, me)]
+
+    # Java-style aliases
+    putTrace = put_trace
+
+    def close(self):
+        if self._ctx is not None:
+            self._ctx.close()
+            self._ctx = None

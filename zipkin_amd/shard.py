@@ -1,0 +1,34 @@
+"""Trace sharding across GPUs.
+
+Traces are independent, so each rank links its own traces; the low 64 bits of
+the trace id pick the rank, because getDependencies groups by lowTraceId
+(InMemoryStorage.java:163, 330, 465-467): sharding on the full 128-bit id
+would split mixed 64/128-bit traces. The only exchange is one sum of the
+per-rank S x S count tables (DependencyLinker.merge semantics, :189-204).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+_M1, _M2, _G = np.uint64(0xBF58476D1CE4E5B9), np.uint64(0x94D049BB133111EB), np.uint64(0x9E3779B97F4A7C15)
+
+
+def splitmix64(x: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        z = np.asarray(x, np.uint64) + _G
+        z = (z ^ (z >> np.uint64(30))) * _M1
+        z = (z ^ (z >> np.uint64(27))) * _M2
+        return z ^ (z >> np.uint64(31))
+
+
+def shard_of(trace_lo: np.ndarray, n_shards: int) -> np.ndarray:
+    return (splitmix64(trace_lo) % np.uint64(n_shards)).astype(np.int64)
+
+
+def combine_tables(call, err, group=None):
+    """Sums per-rank int64 S x S tables in place (torch tensors) with one all-reduce each:
+    RCCL over xGMI on GPUs, gloo on CPU."""
+    import torch.distributed as dist
+    dist.all_reduce(call, op=dist.ReduceOp.SUM, group=group)
+    dist.all_reduce(err, op=dist.ReduceOp.SUM, group=group)
+    return call, err

@@ -1,0 +1,186 @@
+"""InMemoryStorage with getDependencies on the MI355X engine.
+
+Drop-in for the parts of zipkin2.storage.InMemoryStorage
+(zipkin/src/main/java/zipkin2/storage/InMemoryStorage.java) that
+SpanStore.getDependencies(endTs, lookback) exercises:
+
+* builder flags strictTraceId / searchEnabled / maxSpanCount (IMS:72-100);
+* ``accept(spans)`` appends in arrival order and evicts the oldest traces past
+  maxSpanCount (IMS:156-211); spans are packed to columns on arrival;
+* ``getDependencies(endTs, lookback)`` groups by the low 64 bits of the trace id
+  (IMS:323-332, 448-467; strictTraceId is ignored here like the reference), keeps
+  the storage order inside a trace (distinct (lowTraceId, timestamp) keys in
+  first-seen order, then insertion order), and hands the CSR-grouped columns to
+  the engine with the QueryRequest.test time window (QueryRequest.java:262-279)
+  evaluated on the device. Returns a single-use Call (Call.java:370-381).
+"""
+from __future__ import annotations
+
+from typing import Callable, Generic, List, Optional, Sequence, TypeVar
+
+import numpy as np
+
+from .columnar import Columns, concat_columns, pack_traces
+from .linker import DependencyLinker
+from .model import DependencyLink, Span
+
+T = TypeVar("T")
+
+
+class IllegalStateException(RuntimeError):
+    pass
+
+
+class Call(Generic[T]):
+    """zipkin2.Call: execute() once (Call.java:156, Base.execute :370-381)."""
+
+    def __init__(self, fn: Callable[[], T]):
+        self._fn = fn
+        self._executed = False
+
+    def execute(self) -> T:
+        if self._executed:
+            raise IllegalStateException("Already Executed")
+        self._executed = True
+        return self._fn()
+
+    def map(self, mapper: Callable[[T], "U"]) -> "Call":
+        return Call(lambda: mapper(self.execute()))
+
+
+class InMemoryStorage:
+    def __init__(self, strict_trace_id: bool = True, search_enabled: bool = True,
+                 max_span_count: int = 500000, device: int = 0):
+        if max_span_count <= 0:
+            raise ValueError("maxSpanCount <= 0")
+        self.strict_trace_id = strict_trace_id
+        self.search_enabled = search_enabled
+        self.max_span_count = max_span_count
+        self.device = device
+        self._linker = DependencyLinker(device)  # owns the dictionaries
+        self._chunks: List[Columns] = []
+        self._cols: Optional[Columns] = None
+        self._alive = np.zeros(0, bool)
+
+    @staticmethod
+    def new_builder():
+        return _Builder()
+
+    newBuilder = new_builder
+
+    def _columns(self) -> Columns:
+        if self._chunks:
+            parts = ([self._cols] if self._cols is not None else []) + self._chunks
+            self._cols = concat_columns(parts)
+            self._chunks = []
+        return self._cols
+
+    def accept(self, spans: Sequence[Span]) -> Call[None]:
+        spans = list(spans)
+
+        def run():
+            if not spans:
+                return None
+            n_now = int(self._alive.sum())
+            self._evict((n_now + len(spans)) - self.max_span_count)
+            # one "trace" per span: grouping happens at query time
+            cols = pack_traces([[s] for s in spans], self._linker.svc, self._linker.ip4, self._linker.ip6)
+            self._chunks.append(cols)
+            self._alive = np.concatenate([self._alive, np.ones(len(spans), bool)])
+            return None
+
+        # the reference accepts synchronously inside accept() (IMS:156-181)
+        run()
+        return Call(lambda: None)
+
+    def _evict(self, to_recover: int):
+        """deleteOldestTrace (IMS:193-211): the last key of TIMESTAMP_DESCENDING is the
+        smallest timestamp, ties broken by the smallest lowTraceId."""
+        if to_recover <= 0:
+            return
+        cols = self._columns()
+        while to_recover > 0 and self._alive.any():
+            idx = np.nonzero(self._alive)[0]
+            ts = cols.timestamp[idx]
+            m = ts.min()
+            cand = idx[ts == m]
+            low = cols.trace_lo[cand].min()
+            victims = idx[cols.trace_lo[idx] == low]
+            self._alive[victims] = False
+            to_recover -= len(victims)
+
+    def _grouped(self) -> Columns:
+        """Alive spans grouped by trace_lo, IMS storage order inside each trace."""
+        cols = self._columns()
+        idx = np.nonzero(self._alive)[0]
+        if len(idx) == 0:
+            return None
+        low = cols.trace_lo[idx]
+        ts = cols.timestamp[idx]
+        # first arrival index of each distinct (lowTraceId, timestamp) key
+        keys = np.stack([low, ts.view(np.uint64)], axis=1)
+        _, inv = np.unique(keys, axis=0, return_inverse=True)
+        inv = inv.reshape(-1)
+        first = np.full(inv.max() + 1, np.iinfo(np.int64).max, np.int64)
+        np.minimum.at(first, inv, np.arange(len(idx), dtype=np.int64))
+        order = np.lexsort((np.arange(len(idx)), first[inv], low))
+        sel = idx[order]
+        low_sorted = cols.trace_lo[sel]
+        starts = np.nonzero(np.concatenate([[True], low_sorted[1:] != low_sorted[:-1]]))[0]
+        offsets = np.concatenate([starts, [len(sel)]]).astype(np.uint64)
+        pick = lambda a: np.ascontiguousarray(a[sel])  # noqa: E731
+        return Columns(pick(cols.trace_lo), pick(cols.id), pick(cols.parent_id), pick(cols.local_svc),
+                       pick(cols.remote_svc), pick(cols.local_ip4), pick(cols.local_ip6),
+                       pick(cols.port_flags), pick(cols.timestamp), offsets)
+
+    def get_dependencies(self, end_ts: int, lookback: int) -> Call[List[DependencyLink]]:
+        """SpanStore.getDependencies (SpanStore.java:85; IMS:323-332). Milliseconds."""
+        if end_ts <= 0:
+            raise ValueError("endTs <= 0")
+        if lookback <= 0:
+            raise ValueError("lookback <= 0")
+
+        def run():
+            if not self.search_enabled:
+                return []
+            grouped = self._grouped()
+            if grouped is None:
+                return []
+            linker = DependencyLinker(self.device)
+            linker.svc, linker.ip4, linker.ip6 = self._linker.svc, self._linker.ip4, self._linker.ip6
+            try:
+                ctx = linker._context()
+                ctx.set_window(end_ts, lookback)
+                linker.put_columns(grouped)
+                return linker.link()
+            finally:
+                linker.close()
+
+        return Call(run)
+
+    getDependencies = get_dependencies
+
+    def clear(self):
+        self._chunks, self._cols, self._alive = [], None, np.zeros(0, bool)
+
+
+class _Builder:
+    def __init__(self):
+        self._kw = {}
+
+    def strictTraceId(self, v: bool):
+        self._kw["strict_trace_id"] = v
+        return self
+
+    def searchEnabled(self, v: bool):
+        self._kw["search_enabled"] = v
+        return self
+
+    def maxSpanCount(self, v: int):
+        if v <= 0:
+            raise ValueError("maxSpanCount <= 0")
+        self._kw["max_span_count"] = v
+        return self
+
+    def build(self) -> InMemoryStorage:
+        return InMemoryStorage(**self._kw)

@@ -1,0 +1,128 @@
+"""Synthetic workloads of BASELINE.json via libzdl_synth.so.
+
+Deterministic: splitmix64 streams seeded per trace from ``0x5EED0000 + config``.
+Service ids are their own String-order ranks (names ``svc-00000``...; brokers
+``kafka-0``... sort after them), so rank tables are the identity.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass, fields, replace
+from typing import Optional
+
+import numpy as np
+
+from .columnar import Columns
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SYNTH_PATH = os.path.join(HERE, "libzdl_synth.so")
+
+
+class Params(C.Structure):
+    _fields_ = [
+        ("seed", C.c_uint64), ("n_traces", C.c_uint64), ("n_services", C.c_uint32), ("n_brokers", C.c_uint32),
+        ("max_depth", C.c_uint32), ("size_dist", C.c_uint32), ("lam", C.c_double), ("pareto_alpha", C.c_double),
+        ("max_size", C.c_uint32), ("max_fanout", C.c_uint32), ("zipf_s", C.c_double), ("p_shared", C.c_double),
+        ("p_local", C.c_double), ("p_error", C.c_double), ("p_messaging", C.c_double),
+        ("p_missing_broker", C.c_double), ("p_delete", C.c_double), ("p_extra_root", C.c_double),
+        ("p_uninstrumented", C.c_double), ("p_drop_shared_parent", C.c_double), ("p_split", C.c_double),
+        ("p_root_remote", C.c_double), ("shard", C.c_uint32), ("n_shards", C.c_uint32),
+        ("instances", C.c_uint32), ("reserved", C.c_uint32), ("base_ts_us", C.c_int64),
+    ]
+
+
+@dataclass(frozen=True)
+class Workload:
+    name: str
+    seed: int
+    n_traces: int
+    n_services: int
+    n_brokers: int = 0
+    max_depth: int = 8
+    size_dist: int = 0
+    lam: float = 9.0
+    pareto_alpha: float = 1.2
+    max_size: int = 0
+    max_fanout: int = 0
+    zipf_s: float = 1.0
+    p_shared: float = 0.7
+    p_local: float = 0.15
+    p_error: float = 0.02
+    p_messaging: float = 0.0
+    p_missing_broker: float = 0.0
+    p_delete: float = 0.0
+    p_extra_root: float = 0.0
+    p_uninstrumented: float = 0.0
+    p_drop_shared_parent: float = 0.0
+    p_split: float = 0.0
+    p_root_remote: float = 0.1
+    shard: int = 0
+    n_shards: int = 1
+    instances: int = 2
+    base_ts_us: int = 1704067200000000  # 2024-01-01T00:00:00Z
+
+    @property
+    def total_services(self) -> int:
+        return self.n_services + self.n_brokers
+
+    def scaled(self, n_traces: int) -> "Workload":
+        return replace(self, n_traces=n_traces)
+
+    def sharded(self, shard: int, n_shards: int) -> "Workload":
+        return replace(self, shard=shard, n_shards=n_shards)
+
+    def params(self) -> Params:
+        p = Params()
+        for f in fields(self):
+            if f.name == "name":
+                continue
+            setattr(p, f.name, getattr(self, f.name))
+        return p
+
+
+# BASELINE.json configs; seeds 0x5EED0000 + config number
+C2 = Workload("c2_10M_spans_1M_traces_50_services", 0x5EED0002, 1_000_000, 50)
+C3 = Workload("c3_1B_spans_100M_traces_500_services", 0x5EED0003, 100_000_000, 500)
+C4 = Workload("c4_messaging_stress", 0x5EED0004, 1_000_000, 50, n_brokers=4, p_error=0.05,
+              p_messaging=0.4, p_missing_broker=0.1, p_delete=0.05, p_extra_root=0.03, p_uninstrumented=0.1,
+              p_drop_shared_parent=0.1, p_split=0.05)
+C5 = Workload("c5_high_cardinality_10k_services", 0x5EED0005, 16_000_000, 10_000, max_depth=64, size_dist=1,
+              pareto_alpha=1.2, max_size=200_000, max_fanout=1000, zipf_s=1.1)
+CONFIGS = {"c2": C2, "c3": C3, "c4": C4, "c5": C5}
+
+_lib: Optional[C.CDLL] = None
+
+
+def _synth() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(SYNTH_PATH):
+            raise ImportError(f"{SYNTH_PATH} missing: run __graft_entry__.build()")
+        L = C.CDLL(SYNTH_PATH)
+        L.zdl_synth_sizes.restype = C.c_uint64
+        L.zdl_synth_sizes.argtypes = [C.POINTER(Params), C.c_void_p, C.c_int]
+        L.zdl_synth_fill.restype = None
+        L.zdl_synth_fill.argtypes = [C.POINTER(Params), C.c_void_p] + [C.c_void_p] * 9 + [C.c_int]
+        _lib = L
+    return _lib
+
+
+def generate(w: Workload, threads: int = 0) -> Columns:
+    threads = threads or min(16, os.cpu_count() or 1)
+    L = _synth()
+    p = w.params()
+    off = np.empty(w.n_traces + 1, np.uint64)
+    n = int(L.zdl_synth_sizes(C.byref(p), off.ctypes.data, threads))
+    cols = Columns(np.empty(n, np.uint64), np.empty(n, np.uint64), np.empty(n, np.uint64),
+                   np.empty(n, np.int32), np.empty(n, np.int32), np.empty(n, np.int32), np.empty(n, np.int32),
+                   np.empty(n, np.uint32), np.empty(n, np.int64), off)
+    ptr = lambda a: a.ctypes.data  # noqa: E731
+    L.zdl_synth_fill(C.byref(p), off.ctypes.data, ptr(cols.trace_lo), ptr(cols.id), ptr(cols.parent_id),
+                     ptr(cols.local_svc), ptr(cols.remote_svc), ptr(cols.local_ip4), ptr(cols.local_ip6),
+                     ptr(cols.port_flags), ptr(cols.timestamp), threads)
+    return cols
+
+
+def service_names(w: Workload):
+    return [f"svc-{i:05d}" for i in range(w.n_services)] + [f"zkafka-{i}" for i in range(w.n_brokers)]
