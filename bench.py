@@ -1,0 +1,205 @@
+"""Benchmark: spans/sec linked to DependencyLinks on MI355X (BASELINE.json metric).
+
+One step = one pass of the hot path over one batch already resident in HBM:
+reset the S x S counts, zdl_put_spans_device (k_plan, k_tiles, k_reduce, k_big),
+for N > 1 one RCCL all-reduce of the count tables, then zdl_link (k_compact,
+D2H, sort by service name order) -> the DependencyLink list.
+
+N = 1 runs C2 (10M spans / 1M traces / 50 services). N > 1 is weak scaling:
+every rank links its own C2-sized shard of traces picked by
+splitmix64(trace_lo) % N, and the ranks sum their tables once (RCCL over xGMI).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c4|c5]
+    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "spans/sec linked to DependencyLinks at 1/2/4/8 MI355X; % of HBM roofline"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+BYTES_PER_SPAN = 36            # id 8 + parent_id 8 + 4 x i32 dictionary ids + port_flags 4
+BYTES_PER_TRACE = 8            # CSR offset
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--traces", type=int, default=0, help="override traces per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--cpu-sample-traces", type=int, default=200_000)
+    args = ap.parse_args()
+
+    import torch
+
+    from zipkin_amd import _native as N
+    from zipkin_amd import synth
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", init_method="env://")
+    dev = torch.device("cuda", local)
+
+    w = synth.CONFIGS[args.config]
+    if args.traces:
+        w = w.scaled(args.traces)
+    if world > 1:
+        w = w.sharded(rank, world)
+    t0 = time.time()
+    cols = synth.generate(w)
+    log(f"[rank {rank}] generated {cols.n_spans} spans / {cols.n_traces} traces in {time.time() - t0:.1f}s")
+    S = w.total_services
+
+    names = ("id", "parent_id", "local_svc", "remote_svc", "local_ip4", "local_ip6", "port_flags", "timestamp")
+    dcols = {k: torch.from_numpy(np.ascontiguousarray(getattr(cols, k)).view(
+        np.int64 if getattr(cols, k).dtype.itemsize == 8 else np.int32)).to(dev) for k in names}
+    doff = torch.from_numpy(cols.offsets.view(np.int64)).to(dev)
+    ptrs = {k: v.data_ptr() for k, v in dcols.items()}
+    ptrs["timestamp"] = None
+    torch.cuda.synchronize(dev)
+
+    ctx = N.Context(S, device=local, timing=True)
+    tcall = torch.zeros(S * S, dtype=torch.int64, device=dev)
+    terr = torch.zeros(S * S, dtype=torch.int64, device=dev)
+
+    def step():
+        ctx.reset()
+        ctx.put_spans_device(ptrs, cols.n_spans, doff.data_ptr(), cols.n_traces)
+        if world > 1:
+            ctx.table_export(tcall.data_ptr(), terr.data_ptr())
+            ctx.sync()
+            dist.all_reduce(tcall)
+            dist.all_reduce(terr)
+            torch.cuda.synchronize(dev)
+            ctx.table_import(tcall.data_ptr(), terr.data_ptr())
+        return ctx.link()
+
+    for _ in range(args.warmup):
+        step()
+    tiles_ms, all_ms = [], []
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ctx.sync()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+        kt = ctx.kernel_times()
+        tiles_ms.append(kt.tiles_ms)
+        all_ms.append(kt.plan_ms + kt.tiles_ms + kt.reduce_ms + kt.big_ms + kt.compact_ms)
+    ctx.sync()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    if dist:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+        tot = torch.tensor([cols.n_spans], dtype=torch.int64, device=dev)
+        dist.all_reduce(tot)
+        total_spans = int(tot.item())
+    else:
+        total_spans = cols.n_spans
+
+    p, c, n, e = out
+    parity = None
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_parity:
+        from oracle import ref
+        threads = min(os.cpu_count() or 1, 16)
+        t1 = time.perf_counter()
+        st, op, oc, on, oe = ref.link(cols, threads=threads)
+        t_multi = time.perf_counter() - t1
+        got = sorted(zip(p.tolist(), c.tolist(), n.tolist(), e.tolist()))
+        exp = sorted(zip(op.tolist(), oc.tolist(), on.tolist(), oe.tolist()))
+        parity = "bit-exact" if (st == 0 and got == exp) else "MISMATCH"
+        log(f"parity vs C++ restatement ({threads} threads, {t_multi:.2f}s): {parity}, {len(got)} links")
+        if not args.no_cpu_baseline:
+            k = min(args.cpu_sample_traces, cols.n_traces)
+            m = int(cols.offsets[k])
+            from zipkin_amd.columnar import Columns
+            sample = Columns(*(getattr(cols, f)[:m] for f in ("trace_lo", "id", "parent_id", "local_svc",
+                                                                "remote_svc", "local_ip4", "local_ip6",
+                                                                "port_flags", "timestamp")),
+                             np.ascontiguousarray(cols.offsets[:k + 1]))
+            t1 = time.perf_counter()
+            ref.link(sample, threads=1)
+            t_one = time.perf_counter() - t1
+            cpu = {"value": m / t_one, "unit": "spans/s", "cores": 1, "kind": "port",
+                   "sample": f"first {k} traces ({m} spans) of the same C2 batch, 1 thread = one "
+                             f"DependencyLinker (C++ restatement of the reference algorithm)",
+                   "multi_thread": {"value": cols.n_spans / t_multi, "cores": threads,
+                                    "sample": "whole batch, trace-sharded linkers + merge"}}
+            log(f"cpu baseline: {m / t_one:.3e} spans/s on 1 thread; {cols.n_spans / t_multi:.3e} on {threads}")
+
+    if rank == 0:
+        ms_step = elapsed / args.steps * 1e3
+        tiles = float(np.mean(tiles_ms))
+        e2e = float(np.mean(all_ms))
+        bytes_launch = BYTES_PER_SPAN * cols.n_spans + BYTES_PER_TRACE * (cols.n_traces + 1)
+        achieved = bytes_launch / (tiles * 1e-3) / 1e9
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "pmc_k_tiles.json")
+        if os.path.exists(pmc):
+            try:
+                d = json.load(open(pmc))
+                if d.get("workload") == w.name and d.get("n_spans") == cols.n_spans:
+                    traffic = d.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        line = {
+            "metric": METRIC,
+            "value": total_spans / elapsed * args.steps,
+            "unit": "spans/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic",
+            "config": {"workload": w.name, "spans_per_gpu": cols.n_spans, "traces_per_gpu": cols.n_traces,
+                       "services": S, "parallelism": f"trace-shard x{world}" + (" + RCCL all-reduce" if world > 1 else ""),
+                       "kernel_ms": {"k_tiles": tiles, "hot_path_kernels": e2e},
+                       "hot_path_roofline_frac": bytes_launch / (e2e * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                       "parity": parity, "links": int(len(p))},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "k_tiles", "algorithmic_bytes_per_launch": bytes_launch},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,192 @@
+"""Parity of the HIP engine (through the C ABI) with the oracle.
+
+* the reference's own test vectors (tests/golden/) through the DependencyLinker and
+  InMemoryStorage facades;
+* random corner-case traces vs the Python oracle, including the Q1 NPE;
+* synthetic BASELINE workloads (C2, C4, C5-shaped, windowed) vs the C++ restatement,
+  bit-exact on every (parent, child, callCount, errorCount).
+
+Links are compared as sets: the engine returns them sorted, the reference in
+insertion order; DependencyLinker.merge keeps first-seen order and
+is compared exactly.
+"""
+import random
+
+import numpy as np
+import pytest
+
+from oracle import dl_oracle as O
+from oracle import ref
+from tests.golden_io import check_links, links, load, spans
+from tests.stress import random_trace
+from zipkin_amd import _native as N
+from zipkin_amd import synth
+from zipkin_amd.columnar import Dictionary, pack_traces
+from zipkin_amd.linker import DependencyLinker
+from zipkin_amd.storage import InMemoryStorage
+
+pytestmark = pytest.mark.gpu
+
+DL = load("dependency_linker.json")
+ST = load("storage_dependencies.json")
+
+
+def as_set(ls):
+    return sorted((l.parent, l.child, l.call_count, l.error_count) for l in ls)
+
+
+@pytest.mark.parametrize("case", DL["cases"], ids=lambda c: c["name"])
+def test_golden_dependency_linker(case):
+    if case["mode"] == "log":
+        pytest.skip("asserts FINE log text only")
+    linker = DependencyLinker()
+    for t in case["traces"]:
+        linker.put_trace(spans(t))
+    check_links(linker.link(), case["expect"], "only")
+    linker.close()
+
+
+@pytest.mark.parametrize("case", DL["merge_cases"], ids=lambda c: c["name"])
+def test_golden_merge_exact_order(case):
+    check_links(DependencyLinker.merge(links(case["links"])), case["expect"], case["mode"])
+
+
+@pytest.mark.parametrize("case", ST["cases"], ids=lambda c: c["name"])
+def test_golden_storage(case):
+    store = InMemoryStorage(strict_trace_id=True)
+    for b in case["batches"]:
+        store.accept(spans(b)).execute()
+    for q in case["queries"]:
+        check_links(store.get_dependencies(q["endTs"], q["lookback"]).execute(), q["expect"], "only")
+
+
+def test_linker_reusable_and_call_single_use():
+    t = spans(DL["cases"][1]["traces"][0])
+    linker = DependencyLinker().put_trace(t)
+    assert as_set(linker.link()) == as_set(linker.link())
+    linker.put_trace(t)
+    assert {l.call_count for l in linker.link()} == {2}
+    store = InMemoryStorage()
+    call = store.get_dependencies(1, 1)
+    call.execute()
+    with pytest.raises(Exception, match="Already Executed"):
+        call.execute()
+
+
+@pytest.mark.parametrize("seed", range(300))
+def test_random_traces_vs_python_oracle(seed):
+    r = random.Random(1000 + seed)
+    traces = [random_trace(r) for _ in range(r.randint(1, 5))]
+    ol = O.DependencyLinker()
+    try:
+        for t in traces:
+            ol.put_trace(t)
+        expect = as_set(ol.link())
+    except O.ReferenceNPE:
+        expect = "NPE"
+    gl = DependencyLinker()
+    if expect == "NPE":
+        with pytest.raises(N.ReferenceNullPointerException):
+            gl.put_traces(traces)
+    else:
+        gl.put_traces(traces)
+        assert as_set(gl.link()) == expect
+    gl.close()
+
+
+def _engine_vs_cpp(cols, n_services, window=None, svc_rank=None, ip4_rank=None, ip6_rank=None):
+    ctx = N.Context(n_services)
+    if svc_rank is not None:
+        ctx.set_ranks(N.ZDL_DICT_SERVICE, svc_rank)
+    if ip4_rank is not None:
+        ctx.set_ranks(N.ZDL_DICT_IPV4, ip4_rank)
+    if ip6_rank is not None:
+        ctx.set_ranks(N.ZDL_DICT_IPV6, ip6_rank)
+    if window is not None:
+        ctx.set_window(*window)
+    ctx.put_spans(cols)
+    p, c, n, e = ctx.link()
+    ctx.close()
+    st, op, oc, on, oe = ref.link(cols, svc_rank, ip4_rank, ip6_rank, window=window, threads=8)
+    assert st == 0
+    got = sorted(zip(p.tolist(), c.tolist(), n.tolist(), e.tolist()))
+    exp = sorted(zip(op.tolist(), oc.tolist(), on.tolist(), oe.tolist()))
+    assert got == exp
+    return got
+
+
+def test_random_no_npe_batch_vs_cpp_oracle():
+    r = random.Random(99)
+    traces = [random_trace(r, n=r.randint(1, 40), allow_npe=False) for _ in range(3000)]
+    svc, ip4, ip6 = Dictionary(), Dictionary(), Dictionary()
+    cols = pack_traces(traces, svc, ip4, ip6)
+    _engine_vs_cpp(cols, 64, svc_rank=svc.ranks(), ip4_rank=ip4.ranks(), ip6_rank=ip6.ranks())
+
+
+def test_big_traces_vs_cpp_oracle():
+    """Traces longer than the tile kernel's SMALL_MAX take the big-trace kernel."""
+    r = random.Random(5)
+    traces = [random_trace(r, n=r.choice([129, 300, 1000, 4097]), allow_npe=False, id_pool=r.choice([50, 2000]))
+              for _ in range(12)]
+    traces += [random_trace(r, n=r.randint(1, 20), allow_npe=False) for _ in range(200)]
+    r.shuffle(traces)
+    svc, ip4, ip6 = Dictionary(), Dictionary(), Dictionary()
+    cols = pack_traces(traces, svc, ip4, ip6)
+    _engine_vs_cpp(cols, 64, svc_rank=svc.ranks(), ip4_rank=ip4.ranks(), ip6_rank=ip6.ranks())
+
+
+@pytest.mark.parametrize("n_services", [64, 65, 300])
+def test_dense_and_hash_tables_agree(n_services):
+    r = random.Random(3)
+    traces = [random_trace(r, n=r.randint(1, 30), allow_npe=False) for _ in range(2000)]
+    svc, ip4, ip6 = Dictionary(), Dictionary(), Dictionary()
+    cols = pack_traces(traces, svc, ip4, ip6)
+    _engine_vs_cpp(cols, n_services, svc_rank=svc.ranks(), ip4_rank=ip4.ranks(), ip6_rank=ip6.ranks())
+
+
+def test_c2_synthetic_vs_cpp_oracle():
+    w = synth.C2.scaled(200_000)
+    links = _engine_vs_cpp(synth.generate(w), w.total_services)
+    assert len(links) > 100
+
+
+def test_c4_messaging_stress_vs_cpp_oracle():
+    w = synth.C4.scaled(200_000)
+    _engine_vs_cpp(synth.generate(w), w.total_services)
+
+
+def test_c5_high_cardinality_vs_cpp_oracle():
+    w = synth.C5.scaled(20_000)
+    w = synth.Workload(**{**w.__dict__, "max_size": 20_000})
+    _engine_vs_cpp(synth.generate(w), w.total_services)
+
+
+def test_window_vs_cpp_oracle():
+    w = synth.C2.scaled(100_000)
+    cols = synth.generate(w)
+    base_ms = w.base_ts_us // 1000
+    # traces start at base + t ms; keep roughly the middle third
+    _engine_vs_cpp(cols, w.total_services, window=(base_ms + 66_000, 33_000))
+
+
+def test_accumulates_across_puts_and_reset():
+    w = synth.C2.scaled(50_000)
+    cols = synth.generate(w)
+    ctx = N.Context(w.total_services)
+    ctx.put_spans(cols)
+    p1, c1, n1, e1 = ctx.link()
+    ctx.put_spans(cols)
+    p2, c2, n2, e2 = ctx.link()
+    assert np.array_equal(p1, p2) and np.array_equal(n2, 2 * n1) and np.array_equal(e2, 2 * e1)
+    ctx.reset()
+    assert len(ctx.link()[0]) == 0
+    ctx.close()
+
+
+def test_bad_service_id_is_einval():
+    w = synth.C2.scaled(1000)
+    cols = synth.generate(w)
+    ctx = N.Context(10)  # ids up to 49 present
+    with pytest.raises(N.ZdlError):
+        ctx.put_spans(cols)
+    ctx.close()

@@ -219,7 +219,8 @@ __global__ void __launch_bounds__(WG, 2) k_tiles(Args A) {
   __syncthreads();
 
   for (uint32_t k = blockIdx.x; k < A.n_tiles; k += gridDim.x) {
-    const uint32_t tile_t0 = A.tile_first[k], tile_t1 = A.tile_first[k + 1];
+    const uint32_t tile_t0 = A.tile_first[k];
+    const uint32_t tile_t1 = (uint32_t)min((uint64_t)A.tile_first[k + 1], A.n_traces);
     for (uint32_t c0 = tile_t0; c0 < tile_t1; c0 += MAXT) {
       const uint32_t nT = min((uint32_t)MAXT, tile_t1 - c0);
       // ---- P0: trace extents -> local slot offsets
@@ -237,6 +238,10 @@ __global__ void __launch_bounds__(WG, 2) k_tiles(Args A) {
       if (threadIdx.x < nT) t_loc[threadIdx.x] = loc;
       if (threadIdx.x == 0) t_loc[nT] = total;
       __syncthreads();
+      if (total > (uint32_t)CAP) {  // only reachable with non-monotone device offsets
+        if (threadIdx.x == 0) atomicOr(A.status, ST_BADOFF);
+        continue;
+      }
       // ---- P1: stage the chunk's spans in LDS (coalesced within and across traces)
       for (uint32_t s = threadIdx.x; s < total; s += WG) {
         uint32_t lo = 0, hi = nT;  // last j with t_loc[j] <= s
@@ -381,6 +386,7 @@ __global__ void __launch_bounds__(BIG_WG) k_big(Args A) {
   for (uint32_t bi = blockIdx.x; bi < nbig; bi += gridDim.x) {
     const uint32_t t = A.big_list[bi];
     const uint64_t b = A.off[t];
+    if (A.off[t + 1] < b || A.off[t + 1] > A.n_spans) continue;  // k_plan flagged it
     const int n = (int)(A.off[t + 1] - b);
     View v;
     v.id = A.b_id + b;
@@ -707,9 +713,9 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
     c->grid = std::max(1, cus) * 2;  // two 512-thread workgroups per CU (LDS ~62-75 KB each)
   }
   if (e == hipSuccess) {
-    const int dense = SS <= (size_t)DENSE_MAX;
-    e = hipFuncSetAttribute((const void*)k_tiles, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)TileLds::bytes(c->S, dense));
+    (void)SS;  // the largest carve any context can ask for: dense at S*S == DENSE_MAX, or hash
+    const size_t most = std::max(TileLds::bytes(64, 1), TileLds::bytes(65, 0));
+    e = hipFuncSetAttribute((const void*)k_tiles, hipFuncAttributeMaxDynamicSharedMemorySize, (int)most);
   }
   if (e != hipSuccess) {
     g_create_error = std::string("device init failed: ") + hipGetErrorString(e);
