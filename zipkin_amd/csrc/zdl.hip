@@ -15,6 +15,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -33,6 +34,14 @@ constexpr int BIG_WG = 1024;       // threads per big-trace workgroup
 constexpr int DENSE_MAX = 4096;    // S*S <= DENSE_MAX -> dense LDS counters
 constexpr int HCAP = 2048;         // LDS hash slots otherwise
 constexpr int HPROBE = 64;
+// k_wave: one wave per tile of WT span starts; traces up to WSMALL spans; WIN staged slots
+constexpr int WT = 64;
+constexpr int WSMALL = 64;
+constexpr int WIN = 128;
+constexpr int WPB = 8;              // waves per k_wave workgroup
+constexpr int WDENSE_MAX = 2560;    // S*S <= this -> dense LDS counters in k_wave
+constexpr int WTABLE_BYTES = 24576; // max(8 * WDENSE_MAX, 12 * HCAP)
+static_assert(8 * WDENSE_MAX <= WTABLE_BYTES && 12 * HCAP <= WTABLE_BYTES, "k_wave table carve");
 
 struct Cols {
   const uint64_t* id;
@@ -63,6 +72,9 @@ struct Args {
   const uint32_t* big_list;
   const uint32_t* big_count;
   uint32_t* status;
+  uint32_t small_max;    // traces longer than this are k_big's
+  uint32_t skip;         // timing-only ablation (ZDL_SKIP): 1 rank, 2 merge, 4 resolve, 8 emit, 16 stage-only
+  const uint8_t* flags;  // flags[g] = 1 iff a trace starts at span g (g <= n_spans), zero padded
   // big-trace scratch (HBM), indexed by global span index
   uint64_t* b_id;
   uint64_t* b_pid;
@@ -95,6 +107,21 @@ __global__ void k_plan(const uint64_t* __restrict__ off, uint64_t n_traces, uint
   if (t == n_traces) hi = n_tiles;
   if (hi > n_tiles) hi = n_tiles;
   for (uint64_t k = lo; k <= hi; ++k) tile_first[k] = (uint32_t)t;
+}
+
+// Marks trace starts for k_wave and lists the traces it does not take (> WSMALL spans).
+__global__ void k_plan_flags(const uint64_t* __restrict__ off, uint64_t n_traces, uint64_t n_spans,
+                             uint8_t* __restrict__ flags, uint32_t* __restrict__ big_list,
+                             uint32_t* __restrict__ big_count, uint32_t* __restrict__ status) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t > n_traces) return;
+  const uint64_t o = off[t];
+  if (t < n_traces) {
+    const uint64_t e = off[t + 1];
+    if (e < o || e > n_spans) { atomicOr(status, ST_BADOFF); return; }
+    if (e - o > (uint64_t)WSMALL) big_list[atomicAdd(big_count, 1u)] = (uint32_t)t;
+  }
+  if (o <= n_spans) flags[o] = 1;
 }
 
 // ---------------------------------------------------- LDS accumulation table
@@ -362,15 +389,19 @@ __global__ void __launch_bounds__(WG, 2) k_tiles(Args A) {
   }
 }
 
+#include "zdl_wave.inc"  // k_wave (needs Args, LdsTable)
+
 // ----------------------------------------------------------------- k_reduce
+constexpr int REDUCE_ROWS = 32;  // slab rows summed per thread before one 64-bit atomic
 __global__ void k_reduce(const uint32_t* __restrict__ slab, uint32_t rows, uint32_t SS,
                          unsigned long long* __restrict__ call, unsigned long long* __restrict__ err) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= 2 * SS) return;
+  const uint32_t r0 = blockIdx.y * REDUCE_ROWS, r1 = min(rows, r0 + REDUCE_ROWS);
   unsigned long long sum = 0;
-  for (uint32_t r = 0; r < rows; ++r) sum += slab[(size_t)r * 2 * SS + i];
+  for (uint32_t r = r0; r < r1; ++r) sum += slab[(size_t)r * 2 * SS + i];
   if (sum == 0) return;
-  if (i < SS) call[i] += sum; else err[i - SS] += sum;
+  atomicAdd(i < SS ? &call[i] : &err[i - SS], sum);
 }
 
 // -------------------------------------------------------------------- k_big
@@ -607,6 +638,8 @@ struct zdl_ctx {
   hipStream_t stream = nullptr;
   std::string err;
   int grid = 0;
+  bool block_tiles = false;
+  uint32_t skip = 0;  // ZDL_KERNEL=block: the workgroup-per-tile kernel (A/B only)
   // ranks
   DevBuf<int32_t> rank[3];
   uint32_t nrank[3] = {0, 0, 0};
@@ -615,6 +648,7 @@ struct zdl_ctx {
   DevBuf<uint32_t> status;
   // per-put scratch
   DevBuf<uint32_t> tile_first, big_list, big_count, slab;
+  DevBuf<uint8_t> starts;
   DevBuf<uint64_t> b_id, b_pid;
   DevBuf<int32_t> b_lsvc, b_rsvc, b_ip4, b_ip6, b_parent;
   DevBuf<uint32_t> b_pf, b_perm;
@@ -717,6 +751,16 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
     const size_t most = std::max(TileLds::bytes(64, 1), TileLds::bytes(65, 0));
     e = hipFuncSetAttribute((const void*)k_tiles, hipFuncAttributeMaxDynamicSharedMemorySize, (int)most);
   }
+  for (int d = 0; d < 2 && e == hipSuccess; ++d)
+    for (int w = 0; w < 2 && e == hipSuccess; ++w)
+      e = hipFuncSetAttribute(k_wave_fn(d, w), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)wave_block_bytes(w));
+  if (e == hipSuccess) {
+    const char* k = getenv("ZDL_KERNEL");
+    c->block_tiles = k && std::string(k) == "block";
+    const char* sk = getenv("ZDL_SKIP");
+    c->skip = sk ? (uint32_t)strtoul(sk, nullptr, 0) : 0u;
+  }
   if (e != hipSuccess) {
     g_create_error = std::string("device init failed: ") + hipGetErrorString(e);
     zdl_destroy(c);
@@ -732,6 +776,7 @@ void zdl_destroy(zdl_ctx* c) {
   for (auto& r : c->rank) r.release();
   c->call.release(); c->errc.release(); c->status.release();
   c->tile_first.release(); c->big_list.release(); c->big_count.release(); c->slab.release();
+  c->starts.release();
   c->b_id.release(); c->b_pid.release(); c->b_lsvc.release(); c->b_rsvc.release(); c->b_ip4.release();
   c->b_ip6.release(); c->b_parent.release(); c->b_pf.release(); c->b_perm.release(); c->b_live.release();
   c->b_hasc.release();
@@ -787,13 +832,16 @@ int zdl_put_spans_device(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans,
   if (c->window && !col->timestamp) return fail(c, ZDL_EINVAL, "window set but no timestamp column");
   if (n_traces >= 0xffffffffull || n_spans >= (1ull << 40)) return fail(c, ZDL_EINVAL, "input too large");
   HIP_TRY(c, hipSetDevice(c->device));
-  const uint32_t n_tiles = (uint32_t)((n_spans + TS - 1) / TS);
+  const bool blk = c->block_tiles;
+  const uint32_t n_tiles = (uint32_t)((n_spans + (blk ? TS : WT) - 1) / (blk ? TS : WT));
   const size_t SS = (size_t)c->S * c->S;
-  const int dense = SS <= (size_t)DENSE_MAX;
-  const int grid = (int)std::min<uint32_t>((uint32_t)c->grid, std::max<uint32_t>(n_tiles, 1));
-  HIP_TRY(c, c->tile_first.ensure((size_t)n_tiles + 1));
+  const int dense = SS <= (size_t)(blk ? DENSE_MAX : WDENSE_MAX);
+  const uint32_t units = blk ? n_tiles : (uint32_t)((n_tiles + WPB - 1) / WPB);
+  const int grid = (int)std::min<uint32_t>((uint32_t)c->grid, std::max<uint32_t>(units, 1));
   HIP_TRY(c, c->big_list.ensure(n_traces));
   HIP_TRY(c, c->big_count.ensure(1));
+  if (blk) HIP_TRY(c, c->tile_first.ensure((size_t)n_tiles + 1));
+  else HIP_TRY(c, c->starts.ensure(n_spans + 1 + WIN + 64));
   if (dense) HIP_TRY(c, c->slab.ensure((size_t)grid * 2 * SS));
 
   Args A{};
@@ -817,22 +865,34 @@ int zdl_put_spans_device(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans,
   A.big_list = c->big_list.p;
   A.big_count = c->big_count.p;
   A.status = c->status.p;
+  A.flags = c->starts.p;
+  A.small_max = blk ? SMALL_MAX : WSMALL;
+  A.skip = c->skip;
 
   ev_record(c, 0);
   HIP_TRY(c, hipMemsetAsync(c->big_count.p, 0, 4, c->stream));
-  {
-    const uint64_t threads = n_traces + 1;
+  const uint64_t threads = n_traces + 1;
+  if (blk) {
     hipLaunchKernelGGL(k_plan, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, c->stream, off, n_traces,
                        n_tiles, c->tile_first.p, c->big_list.p, c->big_count.p, c->status.p);
-    HIP_TRY(c, hipGetLastError());
+  } else {
+    HIP_TRY(c, hipMemsetAsync(c->starts.p, 0, n_spans + 1 + WIN + 64, c->stream));
+    hipLaunchKernelGGL(k_plan_flags, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, c->stream, off,
+                       n_traces, n_spans, c->starts.p, c->big_list.p, c->big_count.p, c->status.p);
   }
+  HIP_TRY(c, hipGetLastError());
   ev_record(c, 1);
-  hipLaunchKernelGGL(k_tiles, dim3(grid), dim3(WG), TileLds::bytes(c->S, dense), c->stream, A);
+  if (blk) hipLaunchKernelGGL(k_tiles, dim3(grid), dim3(WG), TileLds::bytes(c->S, dense), c->stream, A);
+  else {
+    void* kargs[] = {&A};
+    HIP_TRY(c, hipLaunchKernel(k_wave_fn(dense, c->window), dim3(grid), dim3(WPB * 64), kargs,
+                               wave_block_bytes(c->window), c->stream));
+  }
   HIP_TRY(c, hipGetLastError());
   ev_record(c, 2);
   if (dense) {
-    hipLaunchKernelGGL(k_reduce, dim3((unsigned)((2 * SS + 255) / 256)), dim3(256), 0, c->stream, c->slab.p,
-                       (uint32_t)grid, (uint32_t)SS, c->call.p, c->errc.p);
+    hipLaunchKernelGGL(k_reduce, dim3((unsigned)((2 * SS + 255) / 256), (unsigned)((grid + REDUCE_ROWS - 1) / REDUCE_ROWS)),
+                       dim3(256), 0, c->stream, c->slab.p, (uint32_t)grid, (uint32_t)SS, c->call.p, c->errc.p);
     HIP_TRY(c, hipGetLastError());
   }
   ev_record(c, 3);

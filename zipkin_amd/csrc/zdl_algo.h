@@ -24,7 +24,8 @@ namespace zdl {
 enum : uint32_t { ST_NPE = 1u, ST_BADSVC = 2u, ST_BADOFF = 4u, ST_IAE = 8u };
 enum : int32_t { PAR_TERMINAL = -1, PAR_NONMEMBER = -3 };
 
-struct View {
+template <class PermT, class ParT>
+struct ViewT {
   uint64_t* id;
   uint64_t* pid;
   int32_t* lsvc;
@@ -32,11 +33,13 @@ struct View {
   int32_t* ip4;
   int32_t* ip6;
   uint32_t* pf;
-  uint32_t* perm;     // position -> slot
-  int32_t* parent;    // position -> parent position | PAR_TERMINAL | PAR_NONMEMBER
+  PermT* perm;        // position -> slot
+  ParT* parent;       // position -> parent position | PAR_TERMINAL | PAR_NONMEMBER
   uint8_t* live;      // position -> 1 if it heads a cleaned span (Trace.merge output)
   uint8_t* haschild;  // position -> 1 if some node's tree parent is this position
 };
+using View = ViewT<uint32_t, int32_t>;   // HBM scratch (big traces)
+using WView = ViewT<uint8_t, int16_t>;   // one wave's 128 LDS slots
 
 struct Ranks {
   const int32_t* svc;
@@ -52,12 +55,14 @@ __device__ __forceinline__ bool err_of(uint32_t pf) { return (pf & ZDL_PF_ERROR)
 __device__ __forceinline__ uint32_t rbits_of(uint32_t pf) { return (pf >> 22) & 7u; }
 __device__ __forceinline__ bool is_shared(uint32_t pf) { return shared_of(pf) == 2u; }
 
-__device__ __forceinline__ bool local_null(const View& v, uint32_t s) {
+template <class V>
+__device__ __forceinline__ bool local_null(const V& v, uint32_t s) {
   return v.lsvc[s] < 0 && v.ip4[s] < 0 && v.ip6[s] < 0 && port_of(v.pf[s]) == 0;
 }
 
 // Endpoint.equals on (serviceName, ipv4, ipv6, port), Endpoint.java:554-563; null == null.
-__device__ __forceinline__ bool local_eq(const View& v, uint32_t a, uint32_t b) {
+template <class V>
+__device__ __forceinline__ bool local_eq(const V& v, uint32_t a, uint32_t b) {
   return v.lsvc[a] == v.lsvc[b] && v.ip4[a] == v.ip4[b] && v.ip6[a] == v.ip6[b] &&
          port_of(v.pf[a]) == port_of(v.pf[b]);
 }
@@ -72,7 +77,8 @@ __device__ __forceinline__ int32_t rank_of(int32_t id, const int32_t* rank, uint
 // which reproduces Collections.sort's stability: (id, shared tri-state null<false<true,
 // local endpoint: null first, then serviceName/ipv4/ipv6 by String order, nulls last;
 // port ignored), then storage order.
-__device__ __forceinline__ bool span_less(const View& v, const Ranks& R, uint32_t a, uint32_t b) {
+template <class V>
+__device__ __forceinline__ bool span_less(const V& v, const Ranks& R, uint32_t a, uint32_t b) {
   const uint64_t ia = v.id[a], ib = v.id[b];
   if (ia != ib) return ia < ib;
   const uint32_t sa = shared_of(v.pf[a]), sb = shared_of(v.pf[b]);
@@ -100,7 +106,8 @@ struct Acc {
   bool err;
 };
 
-__device__ __forceinline__ Acc acc_load(const View& v, uint32_t s) {
+template <class V>
+__device__ __forceinline__ Acc acc_load(const V& v, uint32_t s) {
   const uint32_t pf = v.pf[s];
   Acc a;
   a.pid = v.pid[s];
@@ -116,7 +123,8 @@ __device__ __forceinline__ Acc acc_load(const View& v, uint32_t s) {
   return a;
 }
 
-__device__ __forceinline__ void acc_store(const View& v, uint32_t s, const Acc& a) {
+template <class V>
+__device__ __forceinline__ void acc_store(const V& v, uint32_t s, const Acc& a) {
   v.pid[s] = a.pid;
   v.lsvc[s] = a.lsvc;
   v.ip4[s] = a.ip4;
@@ -128,7 +136,8 @@ __device__ __forceinline__ void acc_store(const View& v, uint32_t s, const Acc& 
 
 // Builder.merge(source): first non-null wins per field; an endpoint merge with a null
 // source dereferences it at the first field the accumulator lacks (quirk Q1 -> NPE).
-__device__ __forceinline__ bool acc_merge(Acc& a, const View& v, uint32_t s) {
+template <class V>
+__device__ __forceinline__ bool acc_merge(Acc& a, const V& v, uint32_t s) {
   bool npe = false;
   const uint32_t pf = v.pf[s];
   if (a.pid == 0) a.pid = v.pid[s];
@@ -167,7 +176,8 @@ __device__ __forceinline__ bool acc_merge(Acc& a, const View& v, uint32_t s) {
 // Trace.merge's greedy scan over one id group [gb, ge) of sorted positions
 // (Trace.java:42-84). Run by one lane. Heads of merge runs become live; the merged
 // span is written over the head's slot. Returns true if the reference would NPE.
-__device__ __forceinline__ bool merge_group(const View& v, int gb, int ge) {
+template <class V>
+__device__ __forceinline__ bool merge_group(const V& v, int gb, int ge) {
   bool npe = false;
   int i = gb;
   while (i < ge) {
@@ -220,7 +230,8 @@ __device__ __forceinline__ bool merge_group(const View& v, int gb, int ge) {
 }
 
 // lower_bound of span id P over positions [tb, te) (ids are sorted by position).
-__device__ __forceinline__ void find_group(const View& v, int tb, int te, uint64_t P, int& gb, int& ge) {
+template <class V>
+__device__ __forceinline__ void find_group(const V& v, int tb, int te, uint64_t P, int& gb, int& ge) {
   int lo = tb, hi = te;
   while (lo < hi) {
     const int mid = (lo + hi) >> 1;
@@ -234,7 +245,8 @@ __device__ __forceinline__ void find_group(const View& v, int tb, int te, uint64
 
 // K2N[Key(P, true, ep)] (SpanNode.java:244-245): the last shared cleaned span with id P
 // whose local endpoint equals the slot `es`'s; -1 when SpanNode.Builder holds no such key.
-__device__ __forceinline__ int last_shared_with_ep(const View& v, int tb, int te, uint64_t P, uint32_t es) {
+template <class V>
+__device__ __forceinline__ int last_shared_with_ep(const V& v, int tb, int te, uint64_t P, uint32_t es) {
   int gb, ge;
   find_group(v, tb, te, P, gb, ge);
   int r = -1;
@@ -245,7 +257,8 @@ __device__ __forceinline__ int last_shared_with_ep(const View& v, int tb, int te
 
 // K2N[Key(P, false, null)] (SpanNode.java:247): the last non-shared cleaned span with id
 // P that is not the root (the root is never put in keyToNode, SpanNode.java:238-240).
-__device__ __forceinline__ int last_nonshared(const View& v, int tb, int te, uint64_t P, int rp) {
+template <class V>
+__device__ __forceinline__ int last_nonshared(const V& v, int tb, int te, uint64_t P, int rp) {
   int gb, ge;
   find_group(v, tb, te, P, gb, ge);
   int r = -1;
@@ -263,7 +276,8 @@ __device__ __forceinline__ int last_nonshared(const View& v, int tb, int te, uin
 //    span) re-inserts it. Its node is the last non-root non-shared span; its parent is
 //    the value of the last write: Key(pid,true,ep) from process(), else index()'s
 //    Key(pid,false,null) of the last non-shared span, else none (-> root).
-__device__ __forceinline__ void resolve_group(const View& v, int tb, int te, int gb, int ge, int rp) {
+template <class V>
+__device__ __forceinline__ void resolve_group(const V& v, int tb, int te, int gb, int ge, int rp) {
   const int root_attach = rp >= 0 ? rp : PAR_TERMINAL;
   int last_ns = -1, last_ns_any = -1, last_w = -1;
   for (int p = gb; p < ge; ++p) {
@@ -303,13 +317,13 @@ __device__ __forceinline__ void resolve_group(const View& v, int tb, int te, int
       par = q >= 0 ? q : root_attach;
     }
   }
-  v.parent[last_ns] = par;
+  v.parent[last_ns] = (decltype(+v.parent[0]))par;
 }
 
 // DependencyLinker.putTrace's per-node rules (DependencyLinker.java:58-148) for the node
 // at position p; `emit(parent_svc, child_svc, is_error)` is addLink.
-template <class Emit>
-__device__ __forceinline__ void link_node(const View& v, int p, int rp, int n, Emit&& emit) {
+template <class V, class Emit>
+__device__ __forceinline__ void link_node(const V& v, int p, int rp, int n, Emit&& emit) {
   // reachability from the root and firstRemoteAncestor (DependencyLinker.java:153-164)
   int q = v.parent[p];
   int ra = -1;
