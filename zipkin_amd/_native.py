@@ -51,7 +51,7 @@ class Links(C.Structure):
 class KernelTimes(C.Structure):
     _fields_ = [("plan_ms", C.c_float), ("tiles_ms", C.c_float), ("big_ms", C.c_float),
                 ("reduce_ms", C.c_float), ("compact_ms", C.c_float), ("n_tiles", C.c_uint32),
-                ("n_big", C.c_uint32), ("grid", C.c_uint32), ("reserved", C.c_uint32)]
+                ("n_big", C.c_uint32), ("grid", C.c_uint32), ("full_ms", C.c_float)]
 
 
 class ZdlError(RuntimeError):

@@ -73,6 +73,8 @@ struct Args {
   const uint32_t* big_count;
   uint32_t* status;
   uint32_t small_max;    // traces longer than this are k_big's
+  uint32_t* cx_list;     // k_wave -> k_wave_full: tiles with a non-simple trace
+  uint32_t* cx_count;
   uint32_t skip;         // timing-only ablation (ZDL_SKIP): 1 rank, 2 merge, 4 resolve, 8 emit, 16 stage-only
   const uint8_t* flags;  // flags[g] = 1 iff a trace starts at span g (g <= n_spans), zero padded
   // big-trace scratch (HBM), indexed by global span index
@@ -649,6 +651,7 @@ struct zdl_ctx {
   // per-put scratch
   DevBuf<uint32_t> tile_first, big_list, big_count, slab;
   DevBuf<uint8_t> starts;
+  DevBuf<uint32_t> cx_list, cx_count;
   DevBuf<uint64_t> b_id, b_pid;
   DevBuf<int32_t> b_lsvc, b_rsvc, b_ip4, b_ip6, b_parent;
   DevBuf<uint32_t> b_pf, b_perm;
@@ -755,6 +758,10 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
     for (int w = 0; w < 2 && e == hipSuccess; ++w)
       e = hipFuncSetAttribute(k_wave_fn(d, w), hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)wave_block_bytes(w));
+  for (int d = 0; d < 2 && e == hipSuccess; ++d)
+    for (int w = 0; w < 2 && e == hipSuccess; ++w)
+      e = hipFuncSetAttribute(k_wave_full_fn(d, w), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)wave_block_bytes(w));
   if (e == hipSuccess) {
     const char* k = getenv("ZDL_KERNEL");
     c->block_tiles = k && std::string(k) == "block";
@@ -777,6 +784,8 @@ void zdl_destroy(zdl_ctx* c) {
   c->call.release(); c->errc.release(); c->status.release();
   c->tile_first.release(); c->big_list.release(); c->big_count.release(); c->slab.release();
   c->starts.release();
+  c->cx_list.release();
+  c->cx_count.release();
   c->b_id.release(); c->b_pid.release(); c->b_lsvc.release(); c->b_rsvc.release(); c->b_ip4.release();
   c->b_ip6.release(); c->b_parent.release(); c->b_pf.release(); c->b_perm.release(); c->b_live.release();
   c->b_hasc.release();
@@ -842,7 +851,11 @@ int zdl_put_spans_device(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans,
   HIP_TRY(c, c->big_count.ensure(1));
   if (blk) HIP_TRY(c, c->tile_first.ensure((size_t)n_tiles + 1));
   else HIP_TRY(c, c->starts.ensure(n_spans + 1 + WIN + 64));
-  if (dense) HIP_TRY(c, c->slab.ensure((size_t)grid * 2 * SS));
+  if (dense) HIP_TRY(c, c->slab.ensure((size_t)grid * 2 * 2 * SS));  // k_wave rows, then k_wave_full rows
+  if (!blk) {
+    HIP_TRY(c, c->cx_list.ensure(n_tiles));
+    HIP_TRY(c, c->cx_count.ensure(1));
+  }
 
   Args A{};
   A.c = Cols{col->id, col->parent_id, col->local_svc, col->remote_svc, col->local_ip4, col->local_ip6,
@@ -868,6 +881,8 @@ int zdl_put_spans_device(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans,
   A.flags = c->starts.p;
   A.small_max = blk ? SMALL_MAX : WSMALL;
   A.skip = c->skip;
+  A.cx_list = c->cx_list.p;
+  A.cx_count = c->cx_count.p;
 
   ev_record(c, 0);
   HIP_TRY(c, hipMemsetAsync(c->big_count.p, 0, 4, c->stream));
@@ -885,14 +900,19 @@ int zdl_put_spans_device(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans,
   if (blk) hipLaunchKernelGGL(k_tiles, dim3(grid), dim3(WG), TileLds::bytes(c->S, dense), c->stream, A);
   else {
     void* kargs[] = {&A};
+    HIP_TRY(c, hipMemsetAsync(c->cx_count.p, 0, 4, c->stream));
     HIP_TRY(c, hipLaunchKernel(k_wave_fn(dense, c->window), dim3(grid), dim3(WPB * 64), kargs,
+                               wave_block_bytes(c->window), c->stream));
+    ev_record(c, 7);
+    HIP_TRY(c, hipLaunchKernel(k_wave_full_fn(dense, c->window), dim3(grid), dim3(WPB * 64), kargs,
                                wave_block_bytes(c->window), c->stream));
   }
   HIP_TRY(c, hipGetLastError());
   ev_record(c, 2);
   if (dense) {
-    hipLaunchKernelGGL(k_reduce, dim3((unsigned)((2 * SS + 255) / 256), (unsigned)((grid + REDUCE_ROWS - 1) / REDUCE_ROWS)),
-                       dim3(256), 0, c->stream, c->slab.p, (uint32_t)grid, (uint32_t)SS, c->call.p, c->errc.p);
+    const uint32_t rows = blk ? (uint32_t)grid : 2u * (uint32_t)grid;
+    hipLaunchKernelGGL(k_reduce, dim3((unsigned)((2 * SS + 255) / 256), (unsigned)((rows + REDUCE_ROWS - 1) / REDUCE_ROWS)),
+                       dim3(256), 0, c->stream, c->slab.p, rows, (uint32_t)SS, c->call.p, c->errc.p);
     HIP_TRY(c, hipGetLastError());
   }
   ev_record(c, 3);
@@ -935,7 +955,8 @@ int zdl_sync(zdl_ctx* c) {
   HIP_TRY(c, hipMemcpy(&st, c->status.p, 4, hipMemcpyDeviceToHost));
   if (c->flags & ZDL_FLAG_TIMING) {
     c->times.plan_ms = ev_ms(c, 0, 1);
-    c->times.tiles_ms = ev_ms(c, 1, 2);
+    c->times.tiles_ms = c->block_tiles ? ev_ms(c, 1, 2) : ev_ms(c, 1, 7);
+    c->times.full_ms = c->block_tiles ? 0.f : ev_ms(c, 7, 2);
     c->times.reduce_ms = ev_ms(c, 2, 3);
     c->times.big_ms = ev_ms(c, 3, 4);
   }

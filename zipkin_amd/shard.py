@@ -32,3 +32,26 @@ def combine_tables(call, err, group=None):
     dist.all_reduce(call, op=dist.ReduceOp.SUM, group=group)
     dist.all_reduce(err, op=dist.ReduceOp.SUM, group=group)
     return call, err
+
+
+def partition_columns(cols, n_shards: int):
+    """Splits CSR-grouped columns into n_shards Columns by trace: whole traces only,
+    shard = splitmix64(trace_lo of the trace's first span) % n_shards, storage order kept."""
+    from .columnar import Columns
+    off = cols.offsets.astype(np.int64)
+    sizes = np.diff(off)
+    first = off[:-1]
+    lo = cols.trace_lo[np.minimum(first, max(cols.n_spans - 1, 0))] if cols.n_spans else np.zeros(len(sizes), np.uint64)
+    shard = shard_of(lo, n_shards)
+    out = []
+    span_shard = np.repeat(shard, sizes)
+    for r in range(n_shards):
+        tsel = shard == r
+        ssel = span_shard == r
+        pick = lambda a: np.ascontiguousarray(a[ssel])  # noqa: E731
+        new_off = np.zeros(int(tsel.sum()) + 1, np.uint64)
+        new_off[1:] = np.cumsum(sizes[tsel]).astype(np.uint64)
+        out.append(Columns(pick(cols.trace_lo), pick(cols.id), pick(cols.parent_id), pick(cols.local_svc),
+                           pick(cols.remote_svc), pick(cols.local_ip4), pick(cols.local_ip6),
+                           pick(cols.port_flags), pick(cols.timestamp), new_off))
+    return out
