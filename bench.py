@@ -165,7 +165,7 @@ def main():
         bytes_launch = BYTES_PER_SPAN * cols.n_spans + BYTES_PER_TRACE * (cols.n_traces + 1)
         achieved = bytes_launch / (tiles * 1e-3) / 1e9
         traffic = None
-        pmc = os.path.join(ROOT, "profiles", "pmc_k_tiles.json")
+        pmc = os.path.join(ROOT, "profiles", "pmc_k_wave.json")
         if os.path.exists(pmc):
             try:
                 d = json.load(open(pmc))
