@@ -75,7 +75,13 @@ struct Args {
   uint32_t small_max;    // traces longer than this are k_big's
   uint32_t* cx_list;     // k_wave -> k_wave_full: tiles with a non-simple trace
   uint32_t* cx_count;
-  uint32_t skip;         // timing-only ablation (ZDL_SKIP): 1 rank, 2 merge, 4 resolve, 8 emit, 16 stage-only
+  unsigned long long* prof;  // ZDL_PROF=1: k_link phase cycles (12 counters)
+  const unsigned long long* bits;  // k_plan_bits -> k_link: trace-start bitmap
+  const uint64_t* big_end;         // k_plan_bits -> k_link: end of the big trace starting in block b
+  uint32_t full_row0;    // first slab row of k_link_full's workgroups
+  uint64_t* cx_win;      // k_link -> k_link_full: (base | P << 48, starts mask) per window
+  uint32_t skip;         // timing-only ablation (ZDL_SKIP). k_tiles: 1 rank, 2 merge, 4 resolve, 8 emit, 16 stage-only;
+                         // k_link: 32 stream only, 64 fields, 128 +hash, 256 +parents, 512 +jumping
   const uint8_t* flags;  // flags[g] = 1 iff a trace starts at span g (g <= n_spans), zero padded
   // big-trace scratch (HBM), indexed by global span index
   uint64_t* b_id;
@@ -392,6 +398,7 @@ __global__ void __launch_bounds__(WG, 2) k_tiles(Args A) {
 }
 
 #include "zdl_wave.inc"  // k_wave (needs Args, LdsTable)
+#include "zdl_link.inc"  // k_link, k_link_full (need zdl_wave.inc's helpers)
 
 // ----------------------------------------------------------------- k_reduce
 constexpr int REDUCE_ROWS = 32;  // slab rows summed per thread before one 64-bit atomic
@@ -640,8 +647,10 @@ struct zdl_ctx {
   hipStream_t stream = nullptr;
   std::string err;
   int grid = 0;
-  bool block_tiles = false;
-  uint32_t skip = 0;  // ZDL_KERNEL=block: the workgroup-per-tile kernel (A/B only)
+  int cus = 0;
+  bool block_tiles = false;  // ZDL_KERNEL=block: the workgroup-per-tile kernel (A/B only)
+  bool wave_tiles = false;   // ZDL_KERNEL=wave: the wave-per-tile kernel (A/B only)
+  uint32_t skip = 0;
   // ranks
   DevBuf<int32_t> rank[3];
   uint32_t nrank[3] = {0, 0, 0};
@@ -652,6 +661,12 @@ struct zdl_ctx {
   DevBuf<uint32_t> tile_first, big_list, big_count, slab;
   DevBuf<uint8_t> starts;
   DevBuf<uint32_t> cx_list, cx_count;
+  DevBuf<uint64_t> cx_win;
+  DevBuf<unsigned long long> bits;
+  DevBuf<uint64_t> big_end;
+  DevBuf<unsigned long long> prof;
+  int prof_on = 0;
+  int check = 0;  // ZDL_CHECK=1: verify the trace-start bitmap on the device
   DevBuf<uint64_t> b_id, b_pid;
   DevBuf<int32_t> b_lsvc, b_rsvc, b_ip4, b_ip6, b_parent;
   DevBuf<uint32_t> b_pf, b_perm;
@@ -702,6 +717,7 @@ int status_code(zdl_ctx* c, uint32_t st) {
   if (st & ST_IAE) return fail(c, ZDL_EREF_IAE, "reference throws IllegalArgumentException");
   if (st & ST_BADSVC) return fail(c, ZDL_EINVAL, "service id >= n_services");
   if (st & ST_BADOFF) return fail(c, ZDL_EINVAL, "trace offsets are not non-decreasing");
+  if (st & ST_INTERNAL) return fail(c, ZDL_EDEVICE, "internal consistency check failed on the device");
   return ZDL_OK;
 }
 
@@ -747,7 +763,8 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
   if (e == hipSuccess) {
     int cus = 0;
     e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
-    c->grid = std::max(1, cus) * 2;  // two 512-thread workgroups per CU (LDS ~62-75 KB each)
+    c->cus = std::max(1, cus);
+    c->grid = c->cus * 2;  // two 512-thread workgroups per CU (LDS ~62-75 KB each)
   }
   if (e == hipSuccess) {
     (void)SS;  // the largest carve any context can ask for: dense at S*S == DENSE_MAX, or hash
@@ -762,9 +779,29 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
     for (int w = 0; w < 2 && e == hipSuccess; ++w)
       e = hipFuncSetAttribute(k_wave_full_fn(d, w), hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)wave_block_bytes(w));
+  for (int d = 0; d < 2 && e == hipSuccess; ++d)
+    for (int w = 0; w < 2 && e == hipSuccess; ++w) {
+      e = hipFuncSetAttribute(k_link_fn(d, w), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)link_block_bytes(w));
+      if (e == hipSuccess && d && !w)
+        e = hipFuncSetAttribute(k_link_fn(1, 0, 1), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)link_block_bytes(0));
+      if (e == hipSuccess)
+        e = hipFuncSetAttribute(k_link_full_fn(d, w), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)wave_block_bytes(w));
+    }
   if (e == hipSuccess) {
     const char* k = getenv("ZDL_KERNEL");
     c->block_tiles = k && std::string(k) == "block";
+    c->wave_tiles = k && std::string(k) == "wave";
+    const char* ce = getenv("ZDL_CHECK");
+    c->check = ce && ce[0] == '1';
+    const char* pe = getenv("ZDL_PROF");
+    c->prof_on = pe && pe[0] == '1';
+    if (c->prof_on) {
+      e = c->prof.ensure(12);
+      if (e == hipSuccess) e = hipMemset(c->prof.p, 0, 12 * 8);
+    }
     const char* sk = getenv("ZDL_SKIP");
     c->skip = sk ? (uint32_t)strtoul(sk, nullptr, 0) : 0u;
   }
@@ -786,6 +823,20 @@ void zdl_destroy(zdl_ctx* c) {
   c->starts.release();
   c->cx_list.release();
   c->cx_count.release();
+  c->cx_win.release();
+  c->bits.release();
+  c->big_end.release();
+  if (c->prof_on && c->prof.p) {
+    unsigned long long h[12] = {};
+    if (hipMemcpy(h, c->prof.p, sizeof h, hipMemcpyDeviceToHost) == hipSuccess) {
+      double tot = 0;
+      for (int k = 0; k < 12; ++k) tot += (double)h[k];
+      fprintf(stderr, "[zdl prof] k_link cycles per phase (all waves, all puts):");
+      for (int k = 0; k < 12; ++k) fprintf(stderr, " %d:%.1f%%", k, tot > 0 ? 100.0 * (double)h[k] / tot : 0.0);
+      fprintf(stderr, " total %.3e\n", tot);
+    }
+  }
+  c->prof.release();
   c->b_id.release(); c->b_pid.release(); c->b_lsvc.release(); c->b_rsvc.release(); c->b_ip4.release();
   c->b_ip6.release(); c->b_parent.release(); c->b_pf.release(); c->b_perm.release(); c->b_live.release();
   c->b_hasc.release();
@@ -831,6 +882,106 @@ int zdl_set_window(zdl_ctx* c, int64_t end_ts_ms, int64_t lookback_ms) {
   return ZDL_OK;
 }
 
+// Default pipeline: k_link streams every trace of <= WSMALL spans, k_link_full re-runs
+// the windows it queued, k_reduce sums the dense per-workgroup tables, k_big takes the
+// traces it listed as longer than WSMALL.
+static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans, const uint64_t* off,
+                          uint64_t n_traces) {
+  const size_t SS = (size_t)c->S * c->S;
+  const int dense = SS <= (size_t)WDENSE_MAX;
+  const int grid = c->grid, lgrid = c->grid;  // k_link: two 8-wave workgroups per CU
+  HIP_TRY(c, c->big_list.ensure(n_traces));
+  HIP_TRY(c, c->big_count.ensure(1));
+  if (dense) HIP_TRY(c, c->slab.ensure((size_t)(lgrid + grid) * 2 * SS));  // k_link rows, then k_link_full rows
+  HIP_TRY(c, c->cx_win.ensure(2 * std::min<uint64_t>(n_traces, n_spans)));
+  HIP_TRY(c, c->cx_count.ensure(1));
+  const size_t words = (size_t)(n_spans >> 6) + 8;  // k_link reads up to 5 words past the last block
+  HIP_TRY(c, c->bits.ensure(words));
+  HIP_TRY(c, c->big_end.ensure(words));
+  Args A{};
+  A.c = Cols{col->id, col->parent_id, col->local_svc, col->remote_svc, col->local_ip4, col->local_ip6,
+             col->port_flags, col->timestamp};
+  A.off = off;
+  A.n_traces = n_traces;
+  A.n_spans = n_spans;
+  A.R = Ranks{c->nrank[0] ? c->rank[0].p : nullptr, c->nrank[1] ? c->rank[1].p : nullptr,
+              c->nrank[2] ? c->rank[2].p : nullptr, c->nrank[0], c->nrank[1], c->nrank[2]};
+  A.S = c->S;
+  A.dense = dense;
+  A.window = c->window;
+  A.win_lo = c->win_lo;
+  A.win_hi = c->win_hi;
+  A.call = c->call.p;
+  A.err = c->errc.p;
+  A.slab = c->slab.p;
+  A.big_list = c->big_list.p;
+  A.big_count = c->big_count.p;
+  A.status = c->status.p;
+  A.small_max = WSMALL;
+  A.cx_count = c->cx_count.p;
+  A.cx_win = c->cx_win.p;
+  A.skip = c->skip;
+  A.prof = c->prof.p;
+  A.bits = c->bits.p;
+  A.big_end = c->big_end.p;
+  void* kargs[] = {&A};
+  ev_record(c, 0);
+  HIP_TRY(c, hipMemsetAsync(c->big_count.p, 0, 4, c->stream));
+  HIP_TRY(c, hipMemsetAsync(c->cx_count.p, 0, 4, c->stream));
+  HIP_TRY(c, hipMemsetAsync(c->bits.p, 0, words * 8, c->stream));
+  hipLaunchKernelGGL(k_plan_bits, dim3((unsigned)((n_traces + 255) / 256)), dim3(256), 0, c->stream, off, n_traces,
+                     n_spans, c->bits.p, c->big_end.p, c->big_list.p, c->big_count.p, c->status.p);
+  HIP_TRY(c, hipGetLastError());
+  ev_record(c, 1);
+  A.full_row0 = (uint32_t)lgrid;
+  HIP_TRY(c, hipLaunchKernel(k_link_fn(dense, c->window, c->prof_on), dim3(lgrid), dim3(lk::waves(c->window) * 64), kargs,
+                             link_block_bytes(c->window), c->stream));
+  if (c->check) {  // after k_link: checks what k_link read
+    const uint64_t nthr = std::max<uint64_t>(n_traces, words);
+    hipLaunchKernelGGL(k_check_bits, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, c->stream, off, n_traces,
+                       n_spans, c->bits.p, c->status.p);
+  }
+  ev_record(c, 7);
+  HIP_TRY(c, hipLaunchKernel(k_link_full_fn(dense, c->window), dim3(grid), dim3(WPB * 64), kargs,
+                             wave_block_bytes(c->window), c->stream));
+  ev_record(c, 2);
+  if (dense) {
+    const uint32_t rows = (uint32_t)(lgrid + grid);
+    hipLaunchKernelGGL(k_reduce, dim3((unsigned)((2 * SS + 255) / 256), (unsigned)((rows + REDUCE_ROWS - 1) / REDUCE_ROWS)),
+                       dim3(256), 0, c->stream, c->slab.p, rows, (uint32_t)SS, c->call.p, c->errc.p);
+    HIP_TRY(c, hipGetLastError());
+  }
+  ev_record(c, 3);
+  HIP_TRY(c, c->b_id.ensure(n_spans));
+  HIP_TRY(c, c->b_pid.ensure(n_spans));
+  HIP_TRY(c, c->b_lsvc.ensure(n_spans));
+  HIP_TRY(c, c->b_rsvc.ensure(n_spans));
+  HIP_TRY(c, c->b_ip4.ensure(n_spans));
+  HIP_TRY(c, c->b_ip6.ensure(n_spans));
+  HIP_TRY(c, c->b_pf.ensure(n_spans));
+  HIP_TRY(c, c->b_perm.ensure(n_spans));
+  HIP_TRY(c, c->b_parent.ensure(n_spans));
+  HIP_TRY(c, c->b_live.ensure(n_spans));
+  HIP_TRY(c, c->b_hasc.ensure(n_spans));
+  A.b_id = c->b_id.p;
+  A.b_pid = c->b_pid.p;
+  A.b_lsvc = c->b_lsvc.p;
+  A.b_rsvc = c->b_rsvc.p;
+  A.b_ip4 = c->b_ip4.p;
+  A.b_ip6 = c->b_ip6.p;
+  A.b_pf = c->b_pf.p;
+  A.b_perm = c->b_perm.p;
+  A.b_parent = c->b_parent.p;
+  A.b_live = c->b_live.p;
+  A.b_haschild = c->b_hasc.p;
+  hipLaunchKernelGGL(k_big, dim3(256), dim3(BIG_WG), 0, c->stream, A);
+  HIP_TRY(c, hipGetLastError());
+  ev_record(c, 4);
+  c->times.n_tiles = 0;
+  c->times.grid = (uint32_t)grid;
+  return ZDL_OK;
+}
+
 int zdl_put_spans_device(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans, const uint64_t* off,
                          uint64_t n_traces) {
   if (!c || !col) return fail(c, ZDL_EINVAL, "null argument");
@@ -841,6 +992,7 @@ int zdl_put_spans_device(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans,
   if (c->window && !col->timestamp) return fail(c, ZDL_EINVAL, "window set but no timestamp column");
   if (n_traces >= 0xffffffffull || n_spans >= (1ull << 40)) return fail(c, ZDL_EINVAL, "input too large");
   HIP_TRY(c, hipSetDevice(c->device));
+  if (!c->block_tiles && !c->wave_tiles) return put_spans_link(c, col, n_spans, off, n_traces);
   const bool blk = c->block_tiles;
   const uint32_t n_tiles = (uint32_t)((n_spans + (blk ? TS : WT) - 1) / (blk ? TS : WT));
   const size_t SS = (size_t)c->S * c->S;

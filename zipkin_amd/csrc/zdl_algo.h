@@ -21,7 +21,7 @@
 
 namespace zdl {
 
-enum : uint32_t { ST_NPE = 1u, ST_BADSVC = 2u, ST_BADOFF = 4u, ST_IAE = 8u };
+enum : uint32_t { ST_NPE = 1u, ST_BADSVC = 2u, ST_BADOFF = 4u, ST_IAE = 8u, ST_INTERNAL = 16u };
 enum : int32_t { PAR_TERMINAL = -1, PAR_NONMEMBER = -3 };
 
 template <class PermT, class ParT>
