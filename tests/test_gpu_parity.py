@@ -190,11 +190,3 @@ def test_bad_service_id_is_einval():
     with pytest.raises(N.ZdlError):
         ctx.put_spans(cols)
     ctx.close()
-
-
-@pytest.mark.parametrize("workload", ["c2", "c4"])
-def test_block_tile_kernel_matches(workload, monkeypatch):
-    """The workgroup-per-tile kernel (ZDL_KERNEL=block, kept for A/B) gives the same links."""
-    monkeypatch.setenv("ZDL_KERNEL", "block")
-    w = synth.CONFIGS[workload].scaled(50_000)
-    _engine_vs_cpp(synth.generate(w), w.total_services)

@@ -1,15 +1,15 @@
 // zdl.hip — MI355X (gfx950) kernels and the C ABI of libzdl.so.
 //
 // Pipeline for one zdl_put_spans over CSR-grouped traces:
-//   k_plan    one pass over the trace offsets: tile -> first trace table, and the
-//             list of traces longer than SMALL_MAX ("big")
-//   k_tiles   persistent workgroups, each owns span tiles of TS spans: the traces
-//             that start in a tile are staged in LDS, sorted per trace, merged,
-//             turned into tree edges and linked; (parent, child) counts
-//             accumulate in an LDS table that is flushed once per workgroup
-//   k_big     one workgroup per big trace, same algorithm with HBM scratch and a
-//             bitonic sort
-//   k_reduce  sums the per-workgroup dense LDS tables into the S x S table
+//   k_plan_bits  one pass over the trace offsets: trace-start bitmap (1 bit per span),
+//                the traces longer than WSMALL and their ends
+//   k_link       persistent waves, each streams a contiguous chunk of traces: windows of
+//                whole traces <= 64 spans are linked in registers + a small LDS hash;
+//                (parent, child) counts accumulate in the workgroup's LDS table
+//   k_link_full  the windows k_link queued (fragments / duplicate ids): full
+//                Trace.merge + SpanNode.Builder emulation, one wave per window
+//   k_reduce     sums the per-workgroup dense LDS tables into the S x S table
+//   k_big        one workgroup per trace longer than WSMALL, HBM scratch, bitonic sort
 // zdl_link compacts the non-zero cells (k_compact) and sorts them by service rank.
 #include <hip/hip_runtime.h>
 
@@ -25,23 +25,14 @@
 
 namespace zdl {
 
-constexpr int TS = 512;            // span range per tile
-constexpr int SMALL_MAX = 128;     // longer traces go to k_big
-constexpr int CAP = TS + SMALL_MAX;  // LDS span slots per tile chunk
-constexpr int MAXT = 256;          // traces per chunk
-constexpr int WG = 512;            // threads per tile workgroup
-constexpr int BIG_WG = 1024;       // threads per big-trace workgroup
-constexpr int DENSE_MAX = 4096;    // S*S <= DENSE_MAX -> dense LDS counters
-constexpr int HCAP = 2048;         // LDS hash slots otherwise
+constexpr int BIG_WG = 1024;        // threads per big-trace workgroup
+constexpr int HCAP = 2048;          // LDS hash slots of the (parent, child) table when S*S is large
 constexpr int HPROBE = 64;
-// k_wave: one wave per tile of WT span starts; traces up to WSMALL spans; WIN staged slots
-constexpr int WT = 64;
-constexpr int WSMALL = 64;
-constexpr int WIN = 128;
-constexpr int WPB = 8;              // waves per k_wave workgroup
-constexpr int WDENSE_MAX = 2560;    // S*S <= this -> dense LDS counters in k_wave
-constexpr int WTABLE_BYTES = 24576; // max(8 * WDENSE_MAX, 12 * HCAP)
-static_assert(8 * WDENSE_MAX <= WTABLE_BYTES && 12 * HCAP <= WTABLE_BYTES, "k_wave table carve");
+constexpr int WSMALL = 64;          // traces up to this many spans are k_link's
+constexpr int WPB = 8;              // waves per k_link_full workgroup
+constexpr int WDENSE_MAX = 2560;    // S*S <= this -> dense u64 LDS cells (call | err << 32)
+constexpr int WTABLE_BYTES = 24576; // max(8 * (WDENSE_MAX + 64 dummy cells), 12 * HCAP)
+static_assert(8 * (WDENSE_MAX + 64) <= WTABLE_BYTES && 12 * HCAP <= WTABLE_BYTES, "LDS table carve");
 
 struct Cols {
   const uint64_t* id;
@@ -59,8 +50,6 @@ struct Args {
   const uint64_t* off;
   uint64_t n_traces;
   uint64_t n_spans;
-  const uint32_t* tile_first;
-  uint32_t n_tiles;
   Ranks R;
   uint32_t S;
   int dense;
@@ -68,21 +57,19 @@ struct Args {
   int64_t win_lo, win_hi;
   unsigned long long* call;
   unsigned long long* err;
-  uint32_t* slab;
+  unsigned long long* slab;  // per-workgroup dense tables, S*S u64 cells a row
   const uint32_t* big_list;
   const uint32_t* big_count;
   uint32_t* status;
   uint32_t small_max;    // traces longer than this are k_big's
-  uint32_t* cx_list;     // k_wave -> k_wave_full: tiles with a non-simple trace
   uint32_t* cx_count;
   unsigned long long* prof;  // ZDL_PROF=1: k_link phase cycles (12 counters)
   const unsigned long long* bits;  // k_plan_bits -> k_link: trace-start bitmap
   const uint64_t* big_end;         // k_plan_bits -> k_link: end of the big trace starting in block b
   uint32_t full_row0;    // first slab row of k_link_full's workgroups
   uint64_t* cx_win;      // k_link -> k_link_full: (base | P << 48, starts mask) per window
-  uint32_t skip;         // timing-only ablation (ZDL_SKIP). k_tiles: 1 rank, 2 merge, 4 resolve, 8 emit, 16 stage-only;
-                         // k_link: 32 stream only, 64 fields, 128 +hash, 256 +parents, 512 +jumping
-  const uint8_t* flags;  // flags[g] = 1 iff a trace starts at span g (g <= n_spans), zero padded
+  uint32_t skip;         // timing-only ablation of k_link (ZDL_SKIP): 32 stream only, 64 fields,
+                         // 128 +hash, 256 +parents, 512 +jumping, 2048 no table adds, 4096 cache-resident
   // big-trace scratch (HBM), indexed by global span index
   uint64_t* b_id;
   uint64_t* b_pid;
@@ -97,325 +84,31 @@ struct Args {
   uint8_t* b_haschild;
 };
 
-// ------------------------------------------------------------------- k_plan
-__global__ void k_plan(const uint64_t* __restrict__ off, uint64_t n_traces, uint32_t n_tiles,
-                       uint32_t* __restrict__ tile_first, uint32_t* __restrict__ big_list,
-                       uint32_t* __restrict__ big_count, uint32_t* __restrict__ status) {
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t > n_traces) return;
-  const uint64_t o = off[t];
-  if (t < n_traces) {
-    const uint64_t e = off[t + 1];
-    if (e < o) { atomicOr(status, ST_BADOFF); return; }
-    if (e - o > (uint64_t)SMALL_MAX) big_list[atomicAdd(big_count, 1u)] = (uint32_t)t;
-  }
-  // tile_first[k] = min{t : off[t] >= k*TS}: trace t owns the k with k*TS in (off[t-1], off[t]]
-  const uint64_t lo = t == 0 ? 0 : off[t - 1] / TS + 1;
-  uint64_t hi = o / TS;
-  if (t == n_traces) hi = n_tiles;
-  if (hi > n_tiles) hi = n_tiles;
-  for (uint64_t k = lo; k <= hi; ++k) tile_first[k] = (uint32_t)t;
-}
-
-// Marks trace starts for k_wave and lists the traces it does not take (> WSMALL spans).
-__global__ void k_plan_flags(const uint64_t* __restrict__ off, uint64_t n_traces, uint64_t n_spans,
-                             uint8_t* __restrict__ flags, uint32_t* __restrict__ big_list,
-                             uint32_t* __restrict__ big_count, uint32_t* __restrict__ status) {
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t > n_traces) return;
-  const uint64_t o = off[t];
-  if (t < n_traces) {
-    const uint64_t e = off[t + 1];
-    if (e < o || e > n_spans) { atomicOr(status, ST_BADOFF); return; }
-    if (e - o > (uint64_t)WSMALL) big_list[atomicAdd(big_count, 1u)] = (uint32_t)t;
-  }
-  if (o <= n_spans) flags[o] = 1;
-}
-
-// ---------------------------------------------------- LDS accumulation table
-struct LdsTable {
-  uint32_t* a;  // dense: call[S*S], err[S*S]; hash: key[HCAP], call[HCAP], err[HCAP]
-  uint32_t S;
-  int dense;
-  unsigned long long* gcall;
-  unsigned long long* gerr;
-  uint32_t* status;
-
-  __device__ __forceinline__ void add(int32_t p, int32_t c, bool e) const {
-    if ((uint32_t)p >= S || (uint32_t)c >= S) { atomicOr(status, ST_BADSVC); return; }
-    const uint32_t idx = (uint32_t)p * S + (uint32_t)c;
-    if (dense) {
-      atomicAdd(&a[idx], 1u);
-      if (e) atomicAdd(&a[S * S + idx], 1u);
-      return;
-    }
-    const uint32_t key = idx + 1u;
-    uint32_t h = (key * 2654435761u) & (HCAP - 1);
-    for (int probe = 0; probe < HPROBE; ++probe) {
-      uint32_t k = a[h];
-      if (k == 0) {
-        k = atomicCAS(&a[h], 0u, key);
-        if (k == 0) k = key;
-      }
-      if (k == key) {
-        atomicAdd(&a[HCAP + h], 1u);
-        if (e) atomicAdd(&a[2 * HCAP + h], 1u);
-        return;
-      }
-      h = (h + 1) & (HCAP - 1);
-    }
-    atomicAdd(&gcall[idx], 1ull);  // LDS table full: straight to HBM
-    if (e) atomicAdd(&gerr[idx], 1ull);
-  }
-};
-
-// Block-wide exclusive scan of one u32 per thread (blockDim.x == WG).
-__device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t* warp_sums, uint32_t& total) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  uint32_t incl = x;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(incl, d, 64);
-    if (lane >= d) incl += y;
-  }
-  if (lane == 63) warp_sums[w] = incl;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t acc = 0;
-    for (int i = 0; i < WG / 64; ++i) {
-      const uint32_t t = warp_sums[i];
-      warp_sums[i] = acc;
-      acc += t;
-    }
-    warp_sums[WG / 64] = acc;
-  }
-  __syncthreads();
-  const uint32_t r = warp_sums[w] + incl - x;
-  total = warp_sums[WG / 64];
-  __syncthreads();
-  return r;
-}
-
-// ------------------------------------------------------------------ k_tiles
-struct TileLds {
-  // byte offsets into the dynamic LDS block; every carve 16-B aligned
-  static constexpr size_t o_id = 0;
-  static constexpr size_t o_pid = o_id + 8 * CAP;
-  static constexpr size_t o_ts = o_pid + 8 * CAP;
-  static constexpr size_t o_lsvc = o_ts + 8 * CAP;
-  static constexpr size_t o_rsvc = o_lsvc + 4 * CAP;
-  static constexpr size_t o_ip4 = o_rsvc + 4 * CAP;
-  static constexpr size_t o_ip6 = o_ip4 + 4 * CAP;
-  static constexpr size_t o_pf = o_ip6 + 4 * CAP;
-  static constexpr size_t o_perm = o_pf + 4 * CAP;
-  static constexpr size_t o_seg = o_perm + 4 * CAP;
-  static constexpr size_t o_parent = o_seg + 4 * CAP;
-  static constexpr size_t o_live = o_parent + 4 * CAP;
-  static constexpr size_t o_hasc = o_live + CAP;
-  static constexpr size_t o_tloc = o_hasc + CAP;
-  static constexpr size_t o_tgoff = o_tloc + 4 * (MAXT + 4);
-  static constexpr size_t o_troot = o_tgoff + 8 * MAXT;
-  static constexpr size_t o_tact = o_troot + 4 * MAXT;
-  static constexpr size_t o_scan = o_tact + 4 * MAXT;
-  static constexpr size_t o_table = o_scan + 4 * 32;
-  static size_t bytes(uint32_t S, int dense) {
-    return o_table + (dense ? (size_t)8 * S * S : (size_t)12 * HCAP);
-  }
-};
-static_assert(TileLds::o_table % 16 == 0, "LDS carve alignment");
-
-__global__ void __launch_bounds__(WG, 2) k_tiles(Args A) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  View v;
-  v.id = (uint64_t*)(lds + TileLds::o_id);
-  v.pid = (uint64_t*)(lds + TileLds::o_pid);
-  v.lsvc = (int32_t*)(lds + TileLds::o_lsvc);
-  v.rsvc = (int32_t*)(lds + TileLds::o_rsvc);
-  v.ip4 = (int32_t*)(lds + TileLds::o_ip4);
-  v.ip6 = (int32_t*)(lds + TileLds::o_ip6);
-  v.pf = (uint32_t*)(lds + TileLds::o_pf);
-  v.perm = (uint32_t*)(lds + TileLds::o_perm);
-  v.parent = (int32_t*)(lds + TileLds::o_parent);
-  v.live = (uint8_t*)(lds + TileLds::o_live);
-  v.haschild = (uint8_t*)(lds + TileLds::o_hasc);
-  int64_t* s_ts = (int64_t*)(lds + TileLds::o_ts);
-  uint32_t* s_seg = (uint32_t*)(lds + TileLds::o_seg);
-  uint32_t* t_loc = (uint32_t*)(lds + TileLds::o_tloc);
-  uint64_t* t_goff = (uint64_t*)(lds + TileLds::o_tgoff);
-  int32_t* t_root = (int32_t*)(lds + TileLds::o_troot);
-  uint32_t* t_act = (uint32_t*)(lds + TileLds::o_tact);
-  uint32_t* scan = (uint32_t*)(lds + TileLds::o_scan);
-  uint32_t* table = (uint32_t*)(lds + TileLds::o_table);
-
-  const uint32_t tab_words = A.dense ? 2 * A.S * A.S : 3 * HCAP;
-  for (uint32_t i = threadIdx.x; i < tab_words; i += WG) table[i] = 0;
-  const LdsTable tab{table, A.S, A.dense, A.call, A.err, A.status};
-  bool npe = false;
-  __syncthreads();
-
-  for (uint32_t k = blockIdx.x; k < A.n_tiles; k += gridDim.x) {
-    const uint32_t tile_t0 = A.tile_first[k];
-    const uint32_t tile_t1 = (uint32_t)min((uint64_t)A.tile_first[k + 1], A.n_traces);
-    for (uint32_t c0 = tile_t0; c0 < tile_t1; c0 += MAXT) {
-      const uint32_t nT = min((uint32_t)MAXT, tile_t1 - c0);
-      // ---- P0: trace extents -> local slot offsets
-      uint32_t len = 0;
-      if (threadIdx.x < nT) {
-        const uint64_t b = A.off[c0 + threadIdx.x], e = A.off[c0 + threadIdx.x + 1];
-        const uint64_t l = e - b;
-        len = l <= (uint64_t)SMALL_MAX ? (uint32_t)l : 0u;  // big traces: k_big
-        t_goff[threadIdx.x] = b;
-        t_root[threadIdx.x] = 0x7fffffff;
-        t_act[threadIdx.x] = 1;
-      }
-      uint32_t total;
-      const uint32_t loc = block_excl_scan(len, scan, total);
-      if (threadIdx.x < nT) t_loc[threadIdx.x] = loc;
-      if (threadIdx.x == 0) t_loc[nT] = total;
-      __syncthreads();
-      if (total > (uint32_t)CAP) {  // only reachable with non-monotone device offsets
-        if (threadIdx.x == 0) atomicOr(A.status, ST_BADOFF);
-        continue;
-      }
-      // ---- P1: stage the chunk's spans in LDS (coalesced within and across traces)
-      for (uint32_t s = threadIdx.x; s < total; s += WG) {
-        uint32_t lo = 0, hi = nT;  // last j with t_loc[j] <= s
-        while (hi - lo > 1) {
-          const uint32_t mid = (lo + hi) >> 1;
-          if (t_loc[mid] <= s) lo = mid; else hi = mid;
-        }
-        const uint64_t g = t_goff[lo] + (s - t_loc[lo]);
-        s_seg[s] = lo;
-        const uint64_t id = A.c.id[g];
-        uint64_t pid = A.c.pid[g];
-        if (pid == id) pid = 0;  // Span.build drops a self parent (Span.java:611-617)
-        v.id[s] = id;
-        v.pid[s] = pid;
-        v.lsvc[s] = A.c.lsvc[g];
-        v.rsvc[s] = A.c.rsvc[g];
-        v.ip4[s] = A.c.ip4[g];
-        v.ip6[s] = A.c.ip6[g];
-        v.pf[s] = A.c.pf[g];
-        if (A.window) s_ts[s] = A.c.ts[g];
-      }
-      __syncthreads();
-      // ---- P2: time window per trace (QueryRequest.test), storage order
-      if (A.window) {
-        if (threadIdx.x < nT) {
-          int64_t ts = 0;
-          for (uint32_t s = t_loc[threadIdx.x]; s < t_loc[threadIdx.x + 1]; ++s) {
-            const int64_t x = s_ts[s];
-            if (x == 0) continue;
-            if (v.pid[s] == 0) { ts = x; break; }
-            if (ts == 0 || ts > x) ts = x;
-          }
-          t_act[threadIdx.x] = window_pass(ts, A.win_lo, A.win_hi) ? 1u : 0u;
-        }
-        __syncthreads();
-      }
-      // ---- P3: per-trace rank sort (Trace.merge's Collections.sort)
-      for (uint32_t s = threadIdx.x; s < total; s += WG) {
-        const uint32_t j = s_seg[s];
-        const uint32_t tb = t_loc[j], te = t_loc[j + 1];
-        uint32_t r = 0;
-        if (t_act[j]) {
-          const uint64_t my = v.id[s];
-          for (uint32_t q = tb; q < te; ++q) {
-            const uint64_t o = v.id[q];
-            if (o < my) ++r;
-            else if (o == my && q != s && span_less(v, A.R, q, s)) ++r;
-          }
-        } else {
-          r = s - tb;
-        }
-        v.perm[tb + r] = s;
-      }
-      __syncthreads();
-      // ---- P4: Trace.merge's greedy merge, one lane per id group
-      for (uint32_t p = threadIdx.x; p < total; p += WG) {
-        const uint32_t j = s_seg[p];
-        const uint32_t tb = t_loc[j], te = t_loc[j + 1];
-        v.haschild[p] = 0;
-        if (!t_act[j]) { v.live[p] = 0; continue; }
-        const uint64_t my = v.id[v.perm[p]];
-        if (p != tb && v.id[v.perm[p - 1]] == my) continue;
-        uint32_t ge = p + 1;
-        while (ge < te && v.id[v.perm[ge]] == my) ++ge;
-        if (ge == p + 1) { v.live[p] = 1; continue; }
-        npe |= merge_group(v, (int)p, (int)ge);
-      }
-      __syncthreads();
-      // ---- P5: the root = first non-shared cleaned span without a parent
-      for (uint32_t p = threadIdx.x; p < total; p += WG) {
-        const uint32_t s = v.perm[p];
-        if (v.live[p] && !is_shared(v.pf[s]) && v.pid[s] == 0) atomicMin(&t_root[s_seg[p]], (int32_t)p);
-      }
-      __syncthreads();
-      // ---- P6: tree edges, one lane per id group
-      for (uint32_t p = threadIdx.x; p < total; p += WG) {
-        const uint32_t j = s_seg[p];
-        if (!t_act[j]) { v.parent[p] = PAR_NONMEMBER; continue; }
-        const uint32_t tb = t_loc[j], te = t_loc[j + 1];
-        const uint64_t my = v.id[v.perm[p]];
-        if (p != tb && v.id[v.perm[p - 1]] == my) continue;
-        uint32_t ge = p + 1;
-        while (ge < te && v.id[v.perm[ge]] == my) ++ge;
-        const int32_t rp = t_root[j] == 0x7fffffff ? -1 : t_root[j];
-        resolve_group(v, (int)tb, (int)te, (int)p, (int)ge, rp);
-      }
-      __syncthreads();
-      // ---- P7: which nodes have children (CLIENT-with-children rule)
-      for (uint32_t p = threadIdx.x; p < total; p += WG) {
-        const int32_t q = v.parent[p];
-        if (q >= 0) v.haschild[q] = 1;
-      }
-      __syncthreads();
-      // ---- P8: breadth-first rules -> addLink into the LDS table
-      for (uint32_t p = threadIdx.x; p < total; p += WG) {
-        if (v.parent[p] == PAR_NONMEMBER) continue;
-        const uint32_t j = s_seg[p];
-        const int32_t rp = t_root[j] == 0x7fffffff ? -1 : t_root[j];
-        link_node(v, (int)p, rp, (int)(t_loc[j + 1] - t_loc[j]),
-                  [&](int32_t a, int32_t b, bool e) { tab.add(a, b, e); });
-      }
-      __syncthreads();
-    }
-  }
-  if (npe) atomicOr(A.status, ST_NPE);
-  // ---- flush: dense -> this workgroup's slab row; hash -> HBM atomics
-  if (A.dense) {
-    uint32_t* row = A.slab + (size_t)blockIdx.x * tab_words;
-    for (uint32_t i = threadIdx.x; i < tab_words; i += WG) row[i] = table[i];
-  } else {
-    for (uint32_t h = threadIdx.x; h < HCAP; h += WG) {
-      const uint32_t key = table[h];
-      if (key == 0) continue;
-      atomicAdd(&A.call[key - 1], (unsigned long long)table[HCAP + h]);
-      const uint32_t e = table[2 * HCAP + h];
-      if (e) atomicAdd(&A.err[key - 1], (unsigned long long)e);
-    }
-  }
-}
-
-#include "zdl_wave.inc"  // k_wave (needs Args, LdsTable)
+#include "zdl_full.inc"  // the full per-window emulation (k_link_full's phases)
 #include "zdl_link.inc"  // k_link, k_link_full (need zdl_wave.inc's helpers)
 
 // ----------------------------------------------------------------- k_reduce
+// Sums the per-workgroup tables (one row of S*S u64 cells each: call count in the low
+// 32 bits, error count in the high 32; a row's counts stay below 2^32) into call / err.
 constexpr int REDUCE_ROWS = 32;  // slab rows summed per thread before one 64-bit atomic
-__global__ void k_reduce(const uint32_t* __restrict__ slab, uint32_t rows, uint32_t SS,
+__global__ void k_reduce(const unsigned long long* __restrict__ slab, uint32_t rows, uint32_t SS,
                          unsigned long long* __restrict__ call, unsigned long long* __restrict__ err) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= 2 * SS) return;
+  if (i >= SS) return;
   const uint32_t r0 = blockIdx.y * REDUCE_ROWS, r1 = min(rows, r0 + REDUCE_ROWS);
-  unsigned long long sum = 0;
-  for (uint32_t r = r0; r < r1; ++r) sum += slab[(size_t)r * 2 * SS + i];
-  if (sum == 0) return;
-  atomicAdd(i < SS ? &call[i] : &err[i - SS], sum);
+  unsigned long long nc = 0, ne = 0;
+  for (uint32_t r = r0; r < r1; ++r) {
+    const unsigned long long v = slab[(size_t)r * SS + i];
+    nc += v & 0xFFFFFFFFull;
+    ne += v >> 32;
+  }
+  if (nc) atomicAdd(&call[i], nc);
+  if (ne) atomicAdd(&err[i], ne);
 }
 
 // -------------------------------------------------------------------- k_big
-// One workgroup per trace longer than SMALL_MAX; arrays live in HBM scratch at the
-// trace's global span offset. Same phases as k_tiles, bitonic sort instead of ranks.
+// One workgroup per trace longer than WSMALL; arrays live in HBM scratch at the trace's
+// global span offset. zdl_algo.h's phases, bitonic sort instead of ranks.
 __device__ __forceinline__ void big_sync() { __syncthreads(); }
 
 __global__ void __launch_bounds__(BIG_WG) k_big(Args A) {
@@ -426,7 +119,7 @@ __global__ void __launch_bounds__(BIG_WG) k_big(Args A) {
   for (uint32_t bi = blockIdx.x; bi < nbig; bi += gridDim.x) {
     const uint32_t t = A.big_list[bi];
     const uint64_t b = A.off[t];
-    if (A.off[t + 1] < b || A.off[t + 1] > A.n_spans) continue;  // k_plan flagged it
+    if (A.off[t + 1] < b || A.off[t + 1] > A.n_spans) continue;  // k_plan_bits flagged it
     const int n = (int)(A.off[t + 1] - b);
     View v;
     v.id = A.b_id + b;
@@ -560,19 +253,63 @@ __global__ void __launch_bounds__(BIG_WG) k_big(Args A) {
 }
 
 // ---------------------------------------------------------------- k_compact
+// zdl_link's output record (24 B), copied to the host in one transfer.
+struct ZLink {
+  int32_t parent, child;
+  int64_t call, err;
+};
+
+// Non-zero cells -> records, in cell order (= (parent id, child id) order): one workgroup,
+// a block-wide exclusive scan of the per-thread non-zero counts. For S*S <= 1024 * 8.
+constexpr int COMPACT_WG = 1024;
+__global__ void __launch_bounds__(COMPACT_WG) k_compact_ordered(const unsigned long long* __restrict__ call,
+                                                                const unsigned long long* __restrict__ err,
+                                                                uint32_t SS, uint32_t S,
+                                                                unsigned long long* __restrict__ count,
+                                                                ZLink* __restrict__ out) {
+  __shared__ uint32_t wsum[COMPACT_WG / 64 + 1];
+  const uint32_t K = (SS + COMPACT_WG - 1) / COMPACT_WG, c0 = threadIdx.x * K;
+  uint32_t nz = 0;
+  for (uint32_t k = 0; k < K; ++k) nz += (c0 + k < SS && call[c0 + k] != 0) ? 1u : 0u;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t incl = nz;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += y;
+  }
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+    for (int i = 0; i < COMPACT_WG / 64; ++i) {
+      const uint32_t t = wsum[i];
+      wsum[i] = acc;
+      acc += t;
+    }
+    wsum[COMPACT_WG / 64] = acc;
+    *count = acc;
+  }
+  __syncthreads();
+  uint32_t o = wsum[w] + incl - nz;
+  for (uint32_t k = 0; k < K; ++k) {
+    const uint32_t i = c0 + k;
+    if (i >= SS) break;
+    const unsigned long long n = call[i];
+    if (n == 0) continue;
+    out[o++] = ZLink{(int32_t)(i / S), (int32_t)(i % S), (int64_t)n, (int64_t)err[i]};
+  }
+}
+
+// Any S: non-zero cells -> records in arbitrary order (the host sorts them).
 __global__ void k_compact(const unsigned long long* __restrict__ call, const unsigned long long* __restrict__ err,
-                          uint64_t SS, uint32_t S, unsigned long long* __restrict__ count,
-                          int32_t* __restrict__ op, int32_t* __restrict__ oc, int64_t* __restrict__ ocall,
-                          int64_t* __restrict__ oerr) {
+                          uint64_t SS, uint32_t S, unsigned long long* __restrict__ count, ZLink* __restrict__ out) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= SS) return;
   const unsigned long long n = call[i];
   if (n == 0) return;
   const unsigned long long w = atomicAdd(count, 1ull);
-  op[w] = (int32_t)(i / S);
-  oc[w] = (int32_t)(i % S);
-  ocall[w] = (int64_t)n;
-  oerr[w] = (int64_t)err[i];
+  out[w] = ZLink{(int32_t)(i / S), (int32_t)(i % S), (int64_t)n, (int64_t)err[i]};
 }
 
 // ---------------------------------------------------------- merge (DL.merge)
@@ -648,9 +385,7 @@ struct zdl_ctx {
   std::string err;
   int grid = 0;
   int cus = 0;
-  bool block_tiles = false;  // ZDL_KERNEL=block: the workgroup-per-tile kernel (A/B only)
-  bool wave_tiles = false;   // ZDL_KERNEL=wave: the wave-per-tile kernel (A/B only)
-  uint32_t skip = 0;
+  uint32_t skip = 0;  // ZDL_SKIP: k_link timing-only ablation bits
   // ranks
   DevBuf<int32_t> rank[3];
   uint32_t nrank[3] = {0, 0, 0};
@@ -658,9 +393,8 @@ struct zdl_ctx {
   DevBuf<unsigned long long> call, errc;
   DevBuf<uint32_t> status;
   // per-put scratch
-  DevBuf<uint32_t> tile_first, big_list, big_count, slab;
-  DevBuf<uint8_t> starts;
-  DevBuf<uint32_t> cx_list, cx_count;
+  DevBuf<uint32_t> big_list, big_count, cx_count;
+  DevBuf<unsigned long long> slab;
   DevBuf<uint64_t> cx_win;
   DevBuf<unsigned long long> bits;
   DevBuf<uint64_t> big_end;
@@ -680,6 +414,10 @@ struct zdl_ctx {
   DevBuf<unsigned long long> count, m_call, m_err, m_first;
   DevBuf<int32_t> o_p, o_c;
   DevBuf<int64_t> o_call, o_err;
+  DevBuf<ZLink> o_links;
+  uint64_t* h_meta = nullptr;  // pinned: link count, status
+  ZLink* h_links = nullptr;    // pinned link records
+  size_t h_links_cap = 0;
   DevBuf<uint64_t> o_first;
   DevBuf<int32_t> mi_p, mi_c;
   DevBuf<int64_t> mi_call, mi_err;
@@ -759,41 +497,26 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
   if (e == hipSuccess) e = hipMemset(c->call.p, 0, SS * 8);
   if (e == hipSuccess) e = hipMemset(c->errc.p, 0, SS * 8);
   if (e == hipSuccess) e = hipMemset(c->status.p, 0, 16);
+  if (e == hipSuccess) e = hipHostMalloc((void**)&c->h_meta, 16, hipHostMallocDefault);
   for (int i = 0; i < 8 && e == hipSuccess; ++i) e = hipEventCreate(&c->ev[i]);
   if (e == hipSuccess) {
     int cus = 0;
     e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
     c->cus = std::max(1, cus);
-    c->grid = c->cus * 2;  // two 512-thread workgroups per CU (LDS ~62-75 KB each)
+    c->grid = c->cus * 2;  // k_link_full: two 512-thread workgroups per CU
   }
-  if (e == hipSuccess) {
-    (void)SS;  // the largest carve any context can ask for: dense at S*S == DENSE_MAX, or hash
-    const size_t most = std::max(TileLds::bytes(64, 1), TileLds::bytes(65, 0));
-    e = hipFuncSetAttribute((const void*)k_tiles, hipFuncAttributeMaxDynamicSharedMemorySize, (int)most);
-  }
-  for (int d = 0; d < 2 && e == hipSuccess; ++d)
-    for (int w = 0; w < 2 && e == hipSuccess; ++w)
-      e = hipFuncSetAttribute(k_wave_fn(d, w), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)wave_block_bytes(w));
-  for (int d = 0; d < 2 && e == hipSuccess; ++d)
-    for (int w = 0; w < 2 && e == hipSuccess; ++w)
-      e = hipFuncSetAttribute(k_wave_full_fn(d, w), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)wave_block_bytes(w));
   for (int d = 0; d < 2 && e == hipSuccess; ++d)
     for (int w = 0; w < 2 && e == hipSuccess; ++w) {
       e = hipFuncSetAttribute(k_link_fn(d, w), hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)link_block_bytes(w));
-      if (e == hipSuccess && d && !w)
-        e = hipFuncSetAttribute(k_link_fn(1, 0, 1), hipFuncAttributeMaxDynamicSharedMemorySize,
+      for (int m = 1; m <= 2 && e == hipSuccess && d && !w; ++m)
+        e = hipFuncSetAttribute(k_link_fn(1, 0, m), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)link_block_bytes(0));
       if (e == hipSuccess)
         e = hipFuncSetAttribute(k_link_full_fn(d, w), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)wave_block_bytes(w));
     }
   if (e == hipSuccess) {
-    const char* k = getenv("ZDL_KERNEL");
-    c->block_tiles = k && std::string(k) == "block";
-    c->wave_tiles = k && std::string(k) == "wave";
     const char* ce = getenv("ZDL_CHECK");
     c->check = ce && ce[0] == '1';
     const char* pe = getenv("ZDL_PROF");
@@ -819,9 +542,7 @@ void zdl_destroy(zdl_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (auto& r : c->rank) r.release();
   c->call.release(); c->errc.release(); c->status.release();
-  c->tile_first.release(); c->big_list.release(); c->big_count.release(); c->slab.release();
-  c->starts.release();
-  c->cx_list.release();
+  c->big_list.release(); c->big_count.release(); c->slab.release();
   c->cx_count.release();
   c->cx_win.release();
   c->bits.release();
@@ -844,6 +565,9 @@ void zdl_destroy(zdl_ctx* c) {
   c->h_ip4.release(); c->h_ip6.release(); c->h_pf.release(); c->h_ts.release();
   c->count.release(); c->m_call.release(); c->m_err.release(); c->m_first.release();
   c->o_p.release(); c->o_c.release(); c->o_call.release(); c->o_err.release(); c->o_first.release();
+  c->o_links.release();
+  if (c->h_meta) (void)hipHostFree(c->h_meta);
+  if (c->h_links) (void)hipHostFree(c->h_links);
   c->mi_p.release(); c->mi_c.release(); c->mi_call.release(); c->mi_err.release();
   for (auto& ev : c->ev)
     if (ev) (void)hipEventDestroy(ev);
@@ -889,10 +613,10 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
                           uint64_t n_traces) {
   const size_t SS = (size_t)c->S * c->S;
   const int dense = SS <= (size_t)WDENSE_MAX;
-  const int grid = c->grid, lgrid = c->grid;  // k_link: two 8-wave workgroups per CU
+  const int grid = c->grid, lgrid = c->cus * lk::wgs_per_cu;  // k_link: three 8-wave workgroups per CU
   HIP_TRY(c, c->big_list.ensure(n_traces));
   HIP_TRY(c, c->big_count.ensure(1));
-  if (dense) HIP_TRY(c, c->slab.ensure((size_t)(lgrid + grid) * 2 * SS));  // k_link rows, then k_link_full rows
+  if (dense) HIP_TRY(c, c->slab.ensure((size_t)(lgrid + grid) * SS));  // k_link rows, then k_link_full rows
   HIP_TRY(c, c->cx_win.ensure(2 * std::min<uint64_t>(n_traces, n_spans)));
   HIP_TRY(c, c->cx_count.ensure(1));
   const size_t words = (size_t)(n_spans >> 6) + 8;  // k_link reads up to 5 words past the last block
@@ -924,7 +648,9 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   A.prof = c->prof.p;
   A.bits = c->bits.p;
   A.big_end = c->big_end.p;
+  const unsigned long long* bits_arg = c->bits.p;
   void* kargs[] = {&A};
+  void* lkargs[] = {&A, &bits_arg};
   ev_record(c, 0);
   HIP_TRY(c, hipMemsetAsync(c->big_count.p, 0, 4, c->stream));
   HIP_TRY(c, hipMemsetAsync(c->cx_count.p, 0, 4, c->stream));
@@ -934,7 +660,7 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   HIP_TRY(c, hipGetLastError());
   ev_record(c, 1);
   A.full_row0 = (uint32_t)lgrid;
-  HIP_TRY(c, hipLaunchKernel(k_link_fn(dense, c->window, c->prof_on), dim3(lgrid), dim3(lk::waves(c->window) * 64), kargs,
+  HIP_TRY(c, hipLaunchKernel(k_link_fn(dense, c->window, c->prof_on ? 1 : (c->skip ? 2 : 0)), dim3(lgrid), dim3(lk::waves(c->window) * 64), lkargs,
                              link_block_bytes(c->window), c->stream));
   if (c->check) {  // after k_link: checks what k_link read
     const uint64_t nthr = std::max<uint64_t>(n_traces, words);
@@ -947,7 +673,7 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   ev_record(c, 2);
   if (dense) {
     const uint32_t rows = (uint32_t)(lgrid + grid);
-    hipLaunchKernelGGL(k_reduce, dim3((unsigned)((2 * SS + 255) / 256), (unsigned)((rows + REDUCE_ROWS - 1) / REDUCE_ROWS)),
+    hipLaunchKernelGGL(k_reduce, dim3((unsigned)((SS + 255) / 256), (unsigned)((rows + REDUCE_ROWS - 1) / REDUCE_ROWS)),
                        dim3(256), 0, c->stream, c->slab.p, rows, (uint32_t)SS, c->call.p, c->errc.p);
     HIP_TRY(c, hipGetLastError());
   }
@@ -992,111 +718,7 @@ int zdl_put_spans_device(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans,
   if (c->window && !col->timestamp) return fail(c, ZDL_EINVAL, "window set but no timestamp column");
   if (n_traces >= 0xffffffffull || n_spans >= (1ull << 40)) return fail(c, ZDL_EINVAL, "input too large");
   HIP_TRY(c, hipSetDevice(c->device));
-  if (!c->block_tiles && !c->wave_tiles) return put_spans_link(c, col, n_spans, off, n_traces);
-  const bool blk = c->block_tiles;
-  const uint32_t n_tiles = (uint32_t)((n_spans + (blk ? TS : WT) - 1) / (blk ? TS : WT));
-  const size_t SS = (size_t)c->S * c->S;
-  const int dense = SS <= (size_t)(blk ? DENSE_MAX : WDENSE_MAX);
-  const uint32_t units = blk ? n_tiles : (uint32_t)((n_tiles + WPB - 1) / WPB);
-  const int grid = (int)std::min<uint32_t>((uint32_t)c->grid, std::max<uint32_t>(units, 1));
-  HIP_TRY(c, c->big_list.ensure(n_traces));
-  HIP_TRY(c, c->big_count.ensure(1));
-  if (blk) HIP_TRY(c, c->tile_first.ensure((size_t)n_tiles + 1));
-  else HIP_TRY(c, c->starts.ensure(n_spans + 1 + WIN + 64));
-  if (dense) HIP_TRY(c, c->slab.ensure((size_t)grid * 2 * 2 * SS));  // k_wave rows, then k_wave_full rows
-  if (!blk) {
-    HIP_TRY(c, c->cx_list.ensure(n_tiles));
-    HIP_TRY(c, c->cx_count.ensure(1));
-  }
-
-  Args A{};
-  A.c = Cols{col->id, col->parent_id, col->local_svc, col->remote_svc, col->local_ip4, col->local_ip6,
-             col->port_flags, col->timestamp};
-  A.off = off;
-  A.n_traces = n_traces;
-  A.n_spans = n_spans;
-  A.tile_first = c->tile_first.p;
-  A.n_tiles = n_tiles;
-  A.R = Ranks{c->nrank[0] ? c->rank[0].p : nullptr, c->nrank[1] ? c->rank[1].p : nullptr,
-              c->nrank[2] ? c->rank[2].p : nullptr, c->nrank[0], c->nrank[1], c->nrank[2]};
-  A.S = c->S;
-  A.dense = dense;
-  A.window = c->window;
-  A.win_lo = c->win_lo;
-  A.win_hi = c->win_hi;
-  A.call = c->call.p;
-  A.err = c->errc.p;
-  A.slab = c->slab.p;
-  A.big_list = c->big_list.p;
-  A.big_count = c->big_count.p;
-  A.status = c->status.p;
-  A.flags = c->starts.p;
-  A.small_max = blk ? SMALL_MAX : WSMALL;
-  A.skip = c->skip;
-  A.cx_list = c->cx_list.p;
-  A.cx_count = c->cx_count.p;
-
-  ev_record(c, 0);
-  HIP_TRY(c, hipMemsetAsync(c->big_count.p, 0, 4, c->stream));
-  const uint64_t threads = n_traces + 1;
-  if (blk) {
-    hipLaunchKernelGGL(k_plan, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, c->stream, off, n_traces,
-                       n_tiles, c->tile_first.p, c->big_list.p, c->big_count.p, c->status.p);
-  } else {
-    HIP_TRY(c, hipMemsetAsync(c->starts.p, 0, n_spans + 1 + WIN + 64, c->stream));
-    hipLaunchKernelGGL(k_plan_flags, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, c->stream, off,
-                       n_traces, n_spans, c->starts.p, c->big_list.p, c->big_count.p, c->status.p);
-  }
-  HIP_TRY(c, hipGetLastError());
-  ev_record(c, 1);
-  if (blk) hipLaunchKernelGGL(k_tiles, dim3(grid), dim3(WG), TileLds::bytes(c->S, dense), c->stream, A);
-  else {
-    void* kargs[] = {&A};
-    HIP_TRY(c, hipMemsetAsync(c->cx_count.p, 0, 4, c->stream));
-    HIP_TRY(c, hipLaunchKernel(k_wave_fn(dense, c->window), dim3(grid), dim3(WPB * 64), kargs,
-                               wave_block_bytes(c->window), c->stream));
-    ev_record(c, 7);
-    HIP_TRY(c, hipLaunchKernel(k_wave_full_fn(dense, c->window), dim3(grid), dim3(WPB * 64), kargs,
-                               wave_block_bytes(c->window), c->stream));
-  }
-  HIP_TRY(c, hipGetLastError());
-  ev_record(c, 2);
-  if (dense) {
-    const uint32_t rows = blk ? (uint32_t)grid : 2u * (uint32_t)grid;
-    hipLaunchKernelGGL(k_reduce, dim3((unsigned)((2 * SS + 255) / 256), (unsigned)((rows + REDUCE_ROWS - 1) / REDUCE_ROWS)),
-                       dim3(256), 0, c->stream, c->slab.p, rows, (uint32_t)SS, c->call.p, c->errc.p);
-    HIP_TRY(c, hipGetLastError());
-  }
-  ev_record(c, 3);
-  // big traces: scratch sized by the whole input (only big-trace spans are touched)
-  HIP_TRY(c, c->b_id.ensure(n_spans));
-  HIP_TRY(c, c->b_pid.ensure(n_spans));
-  HIP_TRY(c, c->b_lsvc.ensure(n_spans));
-  HIP_TRY(c, c->b_rsvc.ensure(n_spans));
-  HIP_TRY(c, c->b_ip4.ensure(n_spans));
-  HIP_TRY(c, c->b_ip6.ensure(n_spans));
-  HIP_TRY(c, c->b_pf.ensure(n_spans));
-  HIP_TRY(c, c->b_perm.ensure(n_spans));
-  HIP_TRY(c, c->b_parent.ensure(n_spans));
-  HIP_TRY(c, c->b_live.ensure(n_spans));
-  HIP_TRY(c, c->b_hasc.ensure(n_spans));
-  A.b_id = c->b_id.p;
-  A.b_pid = c->b_pid.p;
-  A.b_lsvc = c->b_lsvc.p;
-  A.b_rsvc = c->b_rsvc.p;
-  A.b_ip4 = c->b_ip4.p;
-  A.b_ip6 = c->b_ip6.p;
-  A.b_pf = c->b_pf.p;
-  A.b_perm = c->b_perm.p;
-  A.b_parent = c->b_parent.p;
-  A.b_live = c->b_live.p;
-  A.b_haschild = c->b_hasc.p;
-  hipLaunchKernelGGL(k_big, dim3(256), dim3(BIG_WG), 0, c->stream, A);
-  HIP_TRY(c, hipGetLastError());
-  ev_record(c, 4);
-  c->times.n_tiles = n_tiles;
-  c->times.grid = (uint32_t)grid;
-  return ZDL_OK;
+  return put_spans_link(c, col, n_spans, off, n_traces);
 }
 
 int zdl_sync(zdl_ctx* c) {
@@ -1107,8 +729,8 @@ int zdl_sync(zdl_ctx* c) {
   HIP_TRY(c, hipMemcpy(&st, c->status.p, 4, hipMemcpyDeviceToHost));
   if (c->flags & ZDL_FLAG_TIMING) {
     c->times.plan_ms = ev_ms(c, 0, 1);
-    c->times.tiles_ms = c->block_tiles ? ev_ms(c, 1, 2) : ev_ms(c, 1, 7);
-    c->times.full_ms = c->block_tiles ? 0.f : ev_ms(c, 7, 2);
+    c->times.tiles_ms = ev_ms(c, 1, 7);
+    c->times.full_ms = ev_ms(c, 7, 2);
     c->times.reduce_ms = ev_ms(c, 2, 3);
     c->times.big_ms = ev_ms(c, 3, 4);
   }
@@ -1168,8 +790,7 @@ int zdl_reset(zdl_ctx* c) {
   HIP_TRY(c, hipMemsetAsync(c->call.p, 0, SS * 8, c->stream));
   HIP_TRY(c, hipMemsetAsync(c->errc.p, 0, SS * 8, c->stream));
   HIP_TRY(c, hipMemsetAsync(c->status.p, 0, 16, c->stream));
-  HIP_TRY(c, hipStreamSynchronize(c->stream));
-  return ZDL_OK;
+  return ZDL_OK;  // stream-ordered: no host wait
 }
 
 static void sort_output(zdl_ctx* c, size_t n) {
@@ -1201,33 +822,57 @@ int zdl_link(zdl_ctx* c, int order, zdl_links* out) {
   if (order != ZDL_ORDER_SORTED) return fail(c, ZDL_EINVAL, "zdl_link supports ZDL_ORDER_SORTED");
   HIP_TRY(c, hipSetDevice(c->device));
   const uint64_t SS = (uint64_t)c->S * c->S;
-  HIP_TRY(c, c->o_p.ensure(SS));
-  HIP_TRY(c, c->o_c.ensure(SS));
-  HIP_TRY(c, c->o_call.ensure(SS));
-  HIP_TRY(c, c->o_err.ensure(SS));
+  const bool ordered = SS <= (uint64_t)COMPACT_WG * 8;
+  HIP_TRY(c, c->o_links.ensure(SS));
   ev_record(c, 5);
-  HIP_TRY(c, hipMemsetAsync(c->count.p, 0, 8, c->stream));
-  hipLaunchKernelGGL(k_compact, dim3((unsigned)((SS + 255) / 256)), dim3(256), 0, c->stream, c->call.p, c->errc.p,
-                     SS, c->S, c->count.p, c->o_p.p, c->o_c.p, c->o_call.p, c->o_err.p);
+  if (ordered) {
+    hipLaunchKernelGGL(k_compact_ordered, dim3(1), dim3(COMPACT_WG), 0, c->stream, c->call.p, c->errc.p,
+                       (uint32_t)SS, c->S, c->count.p, c->o_links.p);
+  } else {
+    HIP_TRY(c, hipMemsetAsync(c->count.p, 0, 8, c->stream));
+    hipLaunchKernelGGL(k_compact, dim3((unsigned)((SS + 255) / 256)), dim3(256), 0, c->stream, c->call.p, c->errc.p,
+                       SS, c->S, c->count.p, c->o_links.p);
+  }
   HIP_TRY(c, hipGetLastError());
   ev_record(c, 6);
-  unsigned long long n = 0;
-  HIP_TRY(c, hipMemcpyAsync(&n, c->count.p, 8, hipMemcpyDeviceToHost, c->stream));
-  int rc = zdl_sync(c);
+  // one round trip for the count and the status word, one for the records
+  HIP_TRY(c, hipMemcpyAsync(&c->h_meta[0], c->count.p, 8, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(&c->h_meta[1], c->status.p, 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  if (c->flags & ZDL_FLAG_TIMING) {
+    c->times.plan_ms = ev_ms(c, 0, 1);
+    c->times.tiles_ms = ev_ms(c, 1, 7);
+    c->times.full_ms = ev_ms(c, 7, 2);
+    c->times.reduce_ms = ev_ms(c, 2, 3);
+    c->times.big_ms = ev_ms(c, 3, 4);
+    c->times.compact_ms = ev_ms(c, 5, 6);
+  }
+  const int rc = status_code(c, (uint32_t)c->h_meta[1]);
   if (rc != ZDL_OK) return rc;
-  if (c->flags & ZDL_FLAG_TIMING) c->times.compact_ms = ev_ms(c, 5, 6);
+  const size_t n = (size_t)c->h_meta[0];
+  if (n > c->h_links_cap) {
+    if (c->h_links) (void)hipHostFree(c->h_links);
+    c->h_links = nullptr;
+    c->h_links_cap = 0;
+    HIP_TRY(c, hipHostMalloc((void**)&c->h_links, n * sizeof(ZLink), hipHostMallocDefault));
+    c->h_links_cap = n;
+  }
+  if (n) {
+    HIP_TRY(c, hipMemcpyAsync(c->h_links, c->o_links.p, n * sizeof(ZLink), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+  }
   c->out_p.resize(n);
   c->out_c.resize(n);
   c->out_call.resize(n);
   c->out_err.resize(n);
-  if (n) {
-    HIP_TRY(c, hipMemcpyAsync(c->out_p.data(), c->o_p.p, n * 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipMemcpyAsync(c->out_c.data(), c->o_c.p, n * 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipMemcpyAsync(c->out_call.data(), c->o_call.p, n * 8, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipMemcpyAsync(c->out_err.data(), c->o_err.p, n * 8, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+  for (size_t i = 0; i < n; ++i) {
+    c->out_p[i] = c->h_links[i].parent;
+    c->out_c[i] = c->h_links[i].child;
+    c->out_call[i] = c->h_links[i].call;
+    c->out_err[i] = c->h_links[i].err;
   }
-  sort_output(c, n);
+  // cell order is (parent id, child id) order; names order needs the service rank table
+  if (!ordered || c->nrank[0] != 0) sort_output(c, n);
   out->n = n;
   out->parent = c->out_p.data();
   out->child = c->out_c.data();
