@@ -1,9 +1,9 @@
 """Benchmark: spans/sec linked to DependencyLinks on MI355X (BASELINE.json metric).
 
 One step = one pass of the hot path over one batch already resident in HBM:
-reset the S x S counts, zdl_put_spans_device (k_plan, k_tiles, k_reduce, k_big),
-for N > 1 one RCCL all-reduce of the count tables, then zdl_link (k_compact,
-D2H, sort by service name order) -> the DependencyLink list.
+reset the S x S counts, zdl_put_spans_device (k_plan_bits, k_link, k_link_full,
+k_reduce, k_big), for N > 1 one RCCL all-reduce of the count tables, then zdl_link
+(ordered compaction, one D2H of the records) -> the DependencyLink list.
 
 N = 1 runs C2 (10M spans / 1M traces / 50 services). N > 1 is weak scaling:
 every rank links its own C2-sized shard of traces picked by
@@ -27,8 +27,8 @@ sys.path.insert(0, ROOT)
 
 METRIC = "spans/sec linked to DependencyLinks at 1/2/4/8 MI355X; % of HBM roofline"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
-BYTES_PER_SPAN = 36            # id 8 + parent_id 8 + 4 x i32 dictionary ids + port_flags 4
-BYTES_PER_TRACE = 8            # CSR offset
+BYTES_PER_SPAN = 36            # id 8 + parent_id 8 + 4 x i32 dictionary ids + port_flags 4 (k_link)
+BYTES_PER_TRACE = 8            # CSR offset (k_plan_bits)
 
 
 def log(*a):
@@ -162,10 +162,11 @@ def main():
         ms_step = elapsed / args.steps * 1e3
         tiles = float(np.mean(tiles_ms))
         e2e = float(np.mean(all_ms))
-        bytes_launch = BYTES_PER_SPAN * cols.n_spans + BYTES_PER_TRACE * (cols.n_traces + 1)
+        bytes_launch = BYTES_PER_SPAN * cols.n_spans  # what k_link must read: every span once
+        bytes_path = bytes_launch + BYTES_PER_TRACE * (cols.n_traces + 1)
         achieved = bytes_launch / (tiles * 1e-3) / 1e9
         traffic = None
-        pmc = os.path.join(ROOT, "profiles", "pmc_k_wave.json")
+        pmc = os.path.join(ROOT, "profiles", "pmc_k_link.json")
         if os.path.exists(pmc):
             try:
                 d = json.load(open(pmc))
@@ -188,12 +189,12 @@ def main():
             "data": "synthetic",
             "config": {"workload": w.name, "spans_per_gpu": cols.n_spans, "traces_per_gpu": cols.n_traces,
                        "services": S, "parallelism": f"trace-shard x{world}" + (" + RCCL all-reduce" if world > 1 else ""),
-                       "kernel_ms": {"k_wave": tiles, "k_wave_full": float(np.mean(full_ms)), "hot_path_kernels": e2e},
-                       "hot_path_roofline_frac": bytes_launch / (e2e * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                       "kernel_ms": {"k_link": tiles, "k_link_full": float(np.mean(full_ms)), "hot_path_kernels": e2e},
+                       "hot_path_roofline_frac": bytes_path / (e2e * 1e-3) / 1e9 / HBM_PEAK_GBS,
                        "parity": parity, "links": int(len(p))},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_wave", "algorithmic_bytes_per_launch": bytes_launch},
+                         "kernel": "k_link", "algorithmic_bytes_per_launch": bytes_launch},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

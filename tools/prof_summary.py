@@ -1,6 +1,6 @@
 """Copies one GPU session's rocprofv3 output into profiles/ and condenses the PMC passes.
 
-    python tools/prof_summary.py TAG [--kernel k_wave] [--workload c2_...] [--n-spans N]
+    python tools/prof_summary.py TAG [--kernel k_link] [--workload c2_...] [--n-spans N]
 
 Reads gpurun_out/prof_TAG/run_kernel_stats.csv (kernel-trace --stats) and the
 FETCH_SIZE / WRITE_SIZE passes gpurun_out/pmc_{fetch,write}_TAG/run_counter_collection.csv,
@@ -41,7 +41,7 @@ def pmc(path: str) -> dict:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("tag")
-    ap.add_argument("--kernel", default="k_wave")
+    ap.add_argument("--kernel", default="k_link")
     ap.add_argument("--workload", default="c2_10M_spans_1M_traces_50_services")
     ap.add_argument("--n-spans", type=int, default=10001749)
     a = ap.parse_args()
