@@ -107,13 +107,13 @@ typedef struct zdl_links {
 } zdl_links;
 
 typedef struct zdl_kernel_times {
-  float plan_ms;     /* k_plan_flags */
-  float tiles_ms;    /* k_wave: tiles whose traces are all simple */
+  float plan_ms;     /* memsets + k_plan_bits */
+  float tiles_ms;    /* k_link: every trace of <= 64 spans */
   float big_ms;      /* k_big: traces > 64 spans */
   float reduce_ms;   /* k_reduce */
   float compact_ms;  /* k_compact (zdl_link) */
-  uint32_t n_tiles, n_big, grid;
-  float full_ms;     /* k_wave_full: tiles with fragments / duplicate ids */
+  uint32_t n_tiles, n_big, grid;  /* n_tiles: unused (0) */
+  float full_ms;     /* k_link_full: windows with fragments / duplicate ids */
 } zdl_kernel_times;
 
 /* Context lifecycle. zdl_create returns NULL on failure (zdl_create_error() says why). */
