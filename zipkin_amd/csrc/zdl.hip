@@ -63,10 +63,11 @@ struct Args {
   uint32_t* status;
   uint32_t small_max;    // traces longer than this are k_big's
   uint32_t* cx_count;
+  uint32_t* cx_count_next;   // the next put's counters (two slots alternate by put):
+  uint32_t* big_count_next;  // zeroed by this put's last kernels, so no memset is needed
   unsigned long long* prof;  // ZDL_PROF=1: k_link phase cycles (12 counters)
   const unsigned long long* bits;  // k_plan_bits -> k_link: trace-start bitmap
   const uint64_t* big_end;         // k_plan_bits -> k_link: end of the big trace starting in block b
-  uint32_t full_row0;    // first slab row of k_link_full's workgroups
   uint64_t* cx_win;      // k_link -> k_link_full: (base | P << 48, starts mask) per window
   uint32_t skip;         // timing-only ablation of k_link (ZDL_SKIP): 32 stream only, 64 fields,
                          // 128 +hash, 256 +parents, 512 +jumping, 2048 no table adds, 4096 cache-resident
@@ -85,7 +86,7 @@ struct Args {
 };
 
 #include "zdl_full.inc"  // the full per-window emulation (k_link_full's phases)
-#include "zdl_link.inc"  // k_link, k_link_full (need zdl_wave.inc's helpers)
+#include "zdl_link.inc"  // k_link, k_link_full (need zdl_full.inc's helpers)
 
 // ----------------------------------------------------------------- k_reduce
 // Sums the per-workgroup tables (one row of S*S u64 cells each: call count in the low
@@ -115,6 +116,7 @@ __global__ void __launch_bounds__(BIG_WG) k_big(Args A) {
   __shared__ int32_t sh_root;
   __shared__ int sh_act;
   __shared__ int64_t sh_ts_root_idx, sh_ts_min;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *A.big_count_next = 0;
   const uint32_t nbig = *A.big_count;
   for (uint32_t bi = blockIdx.x; bi < nbig; bi += gridDim.x) {
     const uint32_t t = A.big_list[bi];
@@ -393,7 +395,8 @@ struct zdl_ctx {
   DevBuf<unsigned long long> call, errc;
   DevBuf<uint32_t> status;
   // per-put scratch
-  DevBuf<uint32_t> big_list, big_count, cx_count;
+  DevBuf<uint32_t> big_list, counters;  // counters: big[2], cx[2], alternating by put
+  uint32_t epoch = 0;
   DevBuf<unsigned long long> slab;
   DevBuf<uint64_t> cx_win;
   DevBuf<unsigned long long> bits;
@@ -497,6 +500,8 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
   if (e == hipSuccess) e = hipMemset(c->call.p, 0, SS * 8);
   if (e == hipSuccess) e = hipMemset(c->errc.p, 0, SS * 8);
   if (e == hipSuccess) e = hipMemset(c->status.p, 0, 16);
+  if (e == hipSuccess) e = c->counters.ensure(4);
+  if (e == hipSuccess) e = hipMemset(c->counters.p, 0, 16);
   if (e == hipSuccess) e = hipHostMalloc((void**)&c->h_meta, 16, hipHostMallocDefault);
   for (int i = 0; i < 8 && e == hipSuccess; ++i) e = hipEventCreate(&c->ev[i]);
   if (e == hipSuccess) {
@@ -542,8 +547,7 @@ void zdl_destroy(zdl_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (auto& r : c->rank) r.release();
   c->call.release(); c->errc.release(); c->status.release();
-  c->big_list.release(); c->big_count.release(); c->slab.release();
-  c->cx_count.release();
+  c->big_list.release(); c->counters.release(); c->slab.release();
   c->cx_win.release();
   c->bits.release();
   c->big_end.release();
@@ -615,10 +619,8 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   const int dense = SS <= (size_t)WDENSE_MAX;
   const int grid = c->grid, lgrid = c->cus * lk::wgs_per_cu;  // k_link: three 8-wave workgroups per CU
   HIP_TRY(c, c->big_list.ensure(n_traces));
-  HIP_TRY(c, c->big_count.ensure(1));
-  if (dense) HIP_TRY(c, c->slab.ensure((size_t)(lgrid + grid) * SS));  // k_link rows, then k_link_full rows
+  if (dense) HIP_TRY(c, c->slab.ensure((size_t)lgrid * SS));  // one row per k_link workgroup
   HIP_TRY(c, c->cx_win.ensure(2 * std::min<uint64_t>(n_traces, n_spans)));
-  HIP_TRY(c, c->cx_count.ensure(1));
   const size_t words = (size_t)(n_spans >> 6) + 8;  // k_link reads up to 5 words past the last block
   HIP_TRY(c, c->bits.ensure(words));
   HIP_TRY(c, c->big_end.ensure(words));
@@ -639,10 +641,13 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   A.err = c->errc.p;
   A.slab = c->slab.p;
   A.big_list = c->big_list.p;
-  A.big_count = c->big_count.p;
+  const uint32_t ep = c->epoch & 1u;
+  A.big_count = c->counters.p + ep;
+  A.big_count_next = c->counters.p + (ep ^ 1u);
   A.status = c->status.p;
   A.small_max = WSMALL;
-  A.cx_count = c->cx_count.p;
+  A.cx_count = c->counters.p + 2 + ep;
+  A.cx_count_next = c->counters.p + 2 + (ep ^ 1u);
   A.cx_win = c->cx_win.p;
   A.skip = c->skip;
   A.prof = c->prof.p;
@@ -652,14 +657,10 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   void* kargs[] = {&A};
   void* lkargs[] = {&A, &bits_arg};
   ev_record(c, 0);
-  HIP_TRY(c, hipMemsetAsync(c->big_count.p, 0, 4, c->stream));
-  HIP_TRY(c, hipMemsetAsync(c->cx_count.p, 0, 4, c->stream));
-  HIP_TRY(c, hipMemsetAsync(c->bits.p, 0, words * 8, c->stream));
   hipLaunchKernelGGL(k_plan_bits, dim3((unsigned)((n_traces + 255) / 256)), dim3(256), 0, c->stream, off, n_traces,
-                     n_spans, c->bits.p, c->big_end.p, c->big_list.p, c->big_count.p, c->status.p);
+                     n_spans, c->bits.p, (uint64_t)words, c->big_end.p, c->big_list.p, c->counters.p + ep, c->status.p);
   HIP_TRY(c, hipGetLastError());
   ev_record(c, 1);
-  A.full_row0 = (uint32_t)lgrid;
   HIP_TRY(c, hipLaunchKernel(k_link_fn(dense, c->window, c->prof_on ? 1 : (c->skip ? 2 : 0)), dim3(lgrid), dim3(lk::waves(c->window) * 64), lkargs,
                              link_block_bytes(c->window), c->stream));
   if (c->check) {  // after k_link: checks what k_link read
@@ -672,7 +673,7 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
                              wave_block_bytes(c->window), c->stream));
   ev_record(c, 2);
   if (dense) {
-    const uint32_t rows = (uint32_t)(lgrid + grid);
+    const uint32_t rows = (uint32_t)lgrid;
     hipLaunchKernelGGL(k_reduce, dim3((unsigned)((SS + 255) / 256), (unsigned)((rows + REDUCE_ROWS - 1) / REDUCE_ROWS)),
                        dim3(256), 0, c->stream, c->slab.p, rows, (uint32_t)SS, c->call.p, c->errc.p);
     HIP_TRY(c, hipGetLastError());
@@ -703,6 +704,7 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   hipLaunchKernelGGL(k_big, dim3(256), dim3(BIG_WG), 0, c->stream, A);
   HIP_TRY(c, hipGetLastError());
   ev_record(c, 4);
+  ++c->epoch;  // k_link_full and k_big zeroed the other counter slots
   c->times.n_tiles = 0;
   c->times.grid = (uint32_t)grid;
   return ZDL_OK;
@@ -787,9 +789,9 @@ int zdl_reset(zdl_ctx* c) {
   if (!c) return ZDL_EINVAL;
   HIP_TRY(c, hipSetDevice(c->device));
   const size_t SS = (size_t)c->S * c->S;
-  HIP_TRY(c, hipMemsetAsync(c->call.p, 0, SS * 8, c->stream));
-  HIP_TRY(c, hipMemsetAsync(c->errc.p, 0, SS * 8, c->stream));
-  HIP_TRY(c, hipMemsetAsync(c->status.p, 0, 16, c->stream));
+  hipLaunchKernelGGL(k_zero_tables, dim3((unsigned)((SS + 255) / 256)), dim3(256), 0, c->stream, c->call.p,
+                     c->errc.p, (uint64_t)SS, c->status.p);
+  HIP_TRY(c, hipGetLastError());
   return ZDL_OK;  // stream-ordered: no host wait
 }
 
@@ -825,19 +827,20 @@ int zdl_link(zdl_ctx* c, int order, zdl_links* out) {
   const bool ordered = SS <= (uint64_t)COMPACT_WG * 8;
   HIP_TRY(c, c->o_links.ensure(SS));
   ev_record(c, 5);
+  // the record count lands next to the status word: status[0] status, status[2..3] count
+  unsigned long long* cnt = reinterpret_cast<unsigned long long*>(c->status.p + 2);
   if (ordered) {
     hipLaunchKernelGGL(k_compact_ordered, dim3(1), dim3(COMPACT_WG), 0, c->stream, c->call.p, c->errc.p,
-                       (uint32_t)SS, c->S, c->count.p, c->o_links.p);
+                       (uint32_t)SS, c->S, cnt, c->o_links.p);
   } else {
-    HIP_TRY(c, hipMemsetAsync(c->count.p, 0, 8, c->stream));
+    HIP_TRY(c, hipMemsetAsync(cnt, 0, 8, c->stream));
     hipLaunchKernelGGL(k_compact, dim3((unsigned)((SS + 255) / 256)), dim3(256), 0, c->stream, c->call.p, c->errc.p,
-                       SS, c->S, c->count.p, c->o_links.p);
+                       SS, c->S, cnt, c->o_links.p);
   }
   HIP_TRY(c, hipGetLastError());
   ev_record(c, 6);
   // one round trip for the count and the status word, one for the records
-  HIP_TRY(c, hipMemcpyAsync(&c->h_meta[0], c->count.p, 8, hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(c, hipMemcpyAsync(&c->h_meta[1], c->status.p, 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(c->h_meta, c->status.p, 16, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   if (c->flags & ZDL_FLAG_TIMING) {
     c->times.plan_ms = ev_ms(c, 0, 1);
@@ -847,9 +850,9 @@ int zdl_link(zdl_ctx* c, int order, zdl_links* out) {
     c->times.big_ms = ev_ms(c, 3, 4);
     c->times.compact_ms = ev_ms(c, 5, 6);
   }
-  const int rc = status_code(c, (uint32_t)c->h_meta[1]);
+  const int rc = status_code(c, (uint32_t)c->h_meta[0]);
   if (rc != ZDL_OK) return rc;
-  const size_t n = (size_t)c->h_meta[0];
+  const size_t n = (size_t)c->h_meta[1];
   if (n > c->h_links_cap) {
     if (c->h_links) (void)hipHostFree(c->h_links);
     c->h_links = nullptr;

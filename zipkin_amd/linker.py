@@ -23,7 +23,7 @@ from . import _native as N
 from .columnar import Columns, Dictionary, pack_traces
 from .model import DependencyLink, Span
 
-MIN_SERVICES = 64  # S*S <= 4096 keeps the engine on its dense LDS counters
+MIN_SERVICES = 48  # S*S <= 2560 keeps the engine on its dense LDS table (WDENSE_MAX)
 
 
 def _capacity(n: int) -> int:
