@@ -617,7 +617,7 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
                           uint64_t n_traces) {
   const size_t SS = (size_t)c->S * c->S;
   const int dense = SS <= (size_t)WDENSE_MAX;
-  const int grid = c->grid, lgrid = c->cus * lk::wgs_per_cu;  // k_link: three 8-wave workgroups per CU
+  const int grid = c->grid, lgrid = c->cus * lk::wgs_per_cu;  // k_link: two 16-wave workgroups per CU
   HIP_TRY(c, c->big_list.ensure(n_traces));
   if (dense) HIP_TRY(c, c->slab.ensure((size_t)lgrid * SS));  // one row per k_link workgroup
   HIP_TRY(c, c->cx_win.ensure(2 * std::min<uint64_t>(n_traces, n_spans)));
