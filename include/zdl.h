@@ -70,7 +70,9 @@ extern "C" {
 #define ZDL_ORDER_FIRST_SEEN  1  /* only for zdl_merge_links output: DependencyLinker.merge order */
 
 /* ---- context flags ---- */
-#define ZDL_FLAG_TIMING  1u      /* record HIP events around every kernel (zdl_kernel_times) */
+#define ZDL_FLAG_TIMING  1u      /* HIP events around k_link only: zdl_kernel_times.tiles_ms = mean of the
+                                    puts since the previous zdl_get_kernel_times (last <= 64) */
+#define ZDL_FLAG_TIMING_ALL 2u   /* record HIP events around every kernel (all zdl_kernel_times fields) */
 
 /*
  * Span columns, structure of arrays, n_spans entries each. A local endpoint is
@@ -94,7 +96,7 @@ typedef struct zdl_config {
   int32_t  device;      /* HIP device ordinal */
   uint32_t n_services;  /* service dictionary size S; links are counted in an S x S table */
   uint32_t flags;       /* ZDL_FLAG_* */
-  uint32_t reserved;
+  uint32_t timing_stride; /* ZDL_FLAG_TIMING: time k_link on every stride-th put (0, 1: every put) */
 } zdl_config;
 
 /* Links owned by the context; valid until the next zdl_link/zdl_merge_links/zdl_destroy. */
@@ -110,9 +112,9 @@ typedef struct zdl_kernel_times {
   float plan_ms;     /* memsets + k_plan_bits */
   float tiles_ms;    /* k_link: every trace of <= 64 spans */
   float big_ms;      /* k_big: traces > 64 spans */
-  float reduce_ms;   /* k_reduce */
+  float reduce_ms;   /* unused (k_link adds its tables itself): the gap between k_link_full and k_big */
   float compact_ms;  /* k_compact (zdl_link) */
-  uint32_t n_tiles, n_big, grid;  /* n_tiles: unused (0) */
+  uint32_t n_tiles, n_big, grid;  /* n_tiles: puts averaged into tiles_ms (ZDL_FLAG_TIMING) */
   float full_ms;     /* k_link_full: windows with fragments / duplicate ids */
 } zdl_kernel_times;
 

@@ -15,6 +15,7 @@ ZDL_OK, ZDL_EINVAL, ZDL_ENOMEM, ZDL_EDEVICE, ZDL_EREF_NPE, ZDL_EREF_IAE = 0, -1,
 ZDL_DICT_SERVICE, ZDL_DICT_IPV4, ZDL_DICT_IPV6 = 0, 1, 2
 ZDL_ORDER_SORTED, ZDL_ORDER_FIRST_SEEN = 0, 1
 ZDL_FLAG_TIMING = 1
+ZDL_FLAG_TIMING_ALL = 2
 
 PF_KIND_SHIFT = 16
 PF_SHARED_SHIFT = 19
@@ -40,7 +41,7 @@ class SpanCols(C.Structure):
 
 class Config(C.Structure):
     _fields_ = [("device", C.c_int32), ("n_services", C.c_uint32), ("flags", C.c_uint32),
-                ("reserved", C.c_uint32)]
+                ("timing_stride", C.c_uint32)]
 
 
 class Links(C.Structure):
@@ -115,9 +116,11 @@ def _ptr(a: Optional[np.ndarray]):
 class Context:
     """One zdl_ctx: a device-resident link-count table for S services."""
 
-    def __init__(self, n_services: int, device: int = 0, timing: bool = False):
+    def __init__(self, n_services: int, device: int = 0, timing: bool = False, timing_all: bool = False,
+                 timing_stride: int = 1):
         L = lib()
-        cfg = Config(device, int(n_services), ZDL_FLAG_TIMING if timing else 0, 0)
+        flags = (ZDL_FLAG_TIMING if timing else 0) | (ZDL_FLAG_TIMING_ALL if timing_all else 0)
+        cfg = Config(device, int(n_services), flags, int(timing_stride))
         h = L.zdl_create(C.byref(cfg))
         if not h:
             raise ZdlError(ZDL_EDEVICE, L.zdl_create_error().decode())

@@ -5,10 +5,10 @@
 //                the traces longer than WSMALL and their ends
 //   k_link       persistent waves, each streams a contiguous chunk of traces: windows of
 //                whole traces <= 64 spans are linked in registers + a small LDS hash;
-//                (parent, child) counts accumulate in the workgroup's LDS table
+//                (parent, child) counts accumulate in the workgroup's LDS table, added
+//                to the S x S table by atomics when the workgroup ends
 //   k_link_full  the windows k_link queued (fragments / duplicate ids): full
 //                Trace.merge + SpanNode.Builder emulation, one wave per window
-//   k_reduce     sums the per-workgroup dense LDS tables into the S x S table
 //   k_big        one workgroup per trace longer than WSMALL, HBM scratch, bitonic sort
 // zdl_link compacts the non-zero cells (k_compact) and sorts them by service rank.
 #include <hip/hip_runtime.h>
@@ -57,7 +57,6 @@ struct Args {
   int64_t win_lo, win_hi;
   unsigned long long* call;
   unsigned long long* err;
-  unsigned long long* slab;  // per-workgroup dense tables, S*S u64 cells a row
   const uint32_t* big_list;
   const uint32_t* big_count;
   uint32_t* status;
@@ -87,25 +86,6 @@ struct Args {
 
 #include "zdl_full.inc"  // the full per-window emulation (k_link_full's phases)
 #include "zdl_link.inc"  // k_link, k_link_full (need zdl_full.inc's helpers)
-
-// ----------------------------------------------------------------- k_reduce
-// Sums the per-workgroup tables (one row of S*S u64 cells each: call count in the low
-// 32 bits, error count in the high 32; a row's counts stay below 2^32) into call / err.
-constexpr int REDUCE_ROWS = 32;  // slab rows summed per thread before one 64-bit atomic
-__global__ void k_reduce(const unsigned long long* __restrict__ slab, uint32_t rows, uint32_t SS,
-                         unsigned long long* __restrict__ call, unsigned long long* __restrict__ err) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= SS) return;
-  const uint32_t r0 = blockIdx.y * REDUCE_ROWS, r1 = min(rows, r0 + REDUCE_ROWS);
-  unsigned long long nc = 0, ne = 0;
-  for (uint32_t r = r0; r < r1; ++r) {
-    const unsigned long long v = slab[(size_t)r * SS + i];
-    nc += v & 0xFFFFFFFFull;
-    ne += v >> 32;
-  }
-  if (nc) atomicAdd(&call[i], nc);
-  if (ne) atomicAdd(&err[i], ne);
-}
 
 // -------------------------------------------------------------------- k_big
 // One workgroup per trace longer than WSMALL; arrays live in HBM scratch at the trace's
@@ -264,11 +244,14 @@ struct ZLink {
 // Non-zero cells -> records, in cell order (= (parent id, child id) order): one workgroup,
 // a block-wide exclusive scan of the per-thread non-zero counts. For S*S <= 1024 * 8.
 constexpr int COMPACT_WG = 1024;
+// Writes straight into the context's mapped pinned buffer: meta[0] = the status word,
+// meta[1] = the record count, then the records (the host reads them after one sync).
 __global__ void __launch_bounds__(COMPACT_WG) k_compact_ordered(const unsigned long long* __restrict__ call,
                                                                 const unsigned long long* __restrict__ err,
                                                                 uint32_t SS, uint32_t S,
-                                                                unsigned long long* __restrict__ count,
-                                                                ZLink* __restrict__ out) {
+                                                                const uint32_t* __restrict__ status,
+                                                                unsigned long long* __restrict__ meta) {
+  ZLink* __restrict__ out = reinterpret_cast<ZLink*>(meta + 2);
   __shared__ uint32_t wsum[COMPACT_WG / 64 + 1];
   const uint32_t K = (SS + COMPACT_WG - 1) / COMPACT_WG, c0 = threadIdx.x * K;
   uint32_t nz = 0;
@@ -290,7 +273,8 @@ __global__ void __launch_bounds__(COMPACT_WG) k_compact_ordered(const unsigned l
       acc += t;
     }
     wsum[COMPACT_WG / 64] = acc;
-    *count = acc;
+    meta[0] = *status;
+    meta[1] = acc;
   }
   __syncthreads();
   uint32_t o = wsum[w] + incl - nz;
@@ -397,7 +381,6 @@ struct zdl_ctx {
   // per-put scratch
   DevBuf<uint32_t> big_list, counters;  // counters: big[2], cx[2], alternating by put
   uint32_t epoch = 0;
-  DevBuf<unsigned long long> slab;
   DevBuf<uint64_t> cx_win;
   DevBuf<unsigned long long> bits;
   DevBuf<uint64_t> big_end;
@@ -419,6 +402,7 @@ struct zdl_ctx {
   DevBuf<int64_t> o_call, o_err;
   DevBuf<ZLink> o_links;
   uint64_t* h_meta = nullptr;  // pinned: link count, status
+  unsigned long long* h_map = nullptr;  // mapped pinned: k_compact_ordered's status, count, records
   ZLink* h_links = nullptr;    // pinned link records
   size_t h_links_cap = 0;
   DevBuf<uint64_t> o_first;
@@ -432,6 +416,12 @@ struct zdl_ctx {
   int64_t win_lo = 0, win_hi = 0;
   // timing
   hipEvent_t ev[8] = {};
+  // ZDL_FLAG_TIMING: a ring of (start, end) event pairs around k_link, one pair per put,
+  // averaged by zdl_get_kernel_times (no per-put host query)
+  static constexpr int LK_RING = 64;
+  hipEvent_t lk_ev[2][LK_RING] = {};
+  uint32_t lk_n = 0;
+  uint32_t lk_stride = 1, lk_puts = 0;  // time every lk_stride-th put
   zdl_kernel_times times = {};
 };
 
@@ -453,6 +443,13 @@ int hip_fail(zdl_ctx* c, hipError_t e, const char* what) {
     if (_e != hipSuccess) return hip_fail((c), _e, #expr); \
   } while (0)
 
+// Every API entry: select the context's device and drop a stale error another call left
+// (hipGetLastError after a launch would otherwise report it as the launch's).
+hipError_t enter(zdl_ctx* c) {
+  (void)hipGetLastError();
+  return hipSetDevice(c->device);
+}
+
 int status_code(zdl_ctx* c, uint32_t st) {
   if (st & ST_NPE) return fail(c, ZDL_EREF_NPE, "reference throws NullPointerException (Span.Builder.merge of a null endpoint)");
   if (st & ST_IAE) return fail(c, ZDL_EREF_IAE, "reference throws IllegalArgumentException");
@@ -462,14 +459,36 @@ int status_code(zdl_ctx* c, uint32_t st) {
   return ZDL_OK;
 }
 
+// Events: 1 / 7 bracket k_link (ZDL_FLAG_TIMING); the others every kernel of the put and
+// the link (ZDL_FLAG_TIMING_ALL). Each event is a packet in the stream, so the light mode
+// keeps the timed step close to an untimed one.
+bool ev_on(const zdl_ctx* c, int i) {
+  (void)i;
+  return (c->flags & ZDL_FLAG_TIMING_ALL) != 0;
+}
+
 void ev_record(zdl_ctx* c, int i) {
-  if (c->flags & ZDL_FLAG_TIMING) (void)hipEventRecord(c->ev[i], c->stream);
+  if (ev_on(c, i)) (void)hipEventRecord(c->ev[i], c->stream);
+  if ((c->flags & ZDL_FLAG_TIMING) && (i == 1 || i == 7) && c->lk_puts % c->lk_stride == 0)
+    (void)hipEventRecord(c->lk_ev[i == 1 ? 0 : 1][(i == 1 ? c->lk_n : c->lk_n++) % zdl_ctx::LK_RING], c->stream);
+  if (i == 7) ++c->lk_puts;
 }
 
 float ev_ms(zdl_ctx* c, int a, int b) {
-  float ms = 0.f;
-  if (hipEventElapsedTime(&ms, c->ev[a], c->ev[b]) != hipSuccess) return -1.f;
+  float ms = -1.f;
+  if (!ev_on(c, a) || !ev_on(c, b)) return -1.f;
+  if (hipEventElapsedTime(&ms, c->ev[a], c->ev[b]) != hipSuccess) ms = -1.f;
+  (void)hipGetLastError();  // an unrecorded event is not an error of the next call
   return ms;
+}
+
+void put_times(zdl_ctx* c) {
+  if (!(c->flags & ZDL_FLAG_TIMING_ALL)) return;
+  c->times.plan_ms = ev_ms(c, 0, 1);
+  c->times.tiles_ms = ev_ms(c, 1, 7);
+  c->times.full_ms = ev_ms(c, 7, 2);
+  c->times.reduce_ms = ev_ms(c, 2, 3);
+  c->times.big_ms = ev_ms(c, 3, 4);
 }
 
 }  // namespace
@@ -490,6 +509,7 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
   c->device = cfg->device;
   c->S = cfg->n_services;
   c->flags = cfg->flags;
+  c->lk_stride = std::max<uint32_t>(1u, cfg->timing_stride);
   hipError_t e = hipSetDevice(c->device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   const size_t SS = (size_t)c->S * c->S;
@@ -503,7 +523,10 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
   if (e == hipSuccess) e = c->counters.ensure(4);
   if (e == hipSuccess) e = hipMemset(c->counters.p, 0, 16);
   if (e == hipSuccess) e = hipHostMalloc((void**)&c->h_meta, 16, hipHostMallocDefault);
-  for (int i = 0; i < 8 && e == hipSuccess; ++i) e = hipEventCreate(&c->ev[i]);
+  // timing-only events: no system-scope fence (cache writeback) between the kernels they bracket
+  for (int i = 0; i < 8 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->ev[i], hipEventDisableSystemFence);
+  for (int i = 0; i < 2 * zdl_ctx::LK_RING && e == hipSuccess && (cfg->flags & ZDL_FLAG_TIMING); ++i)
+    e = hipEventCreateWithFlags(&c->lk_ev[i & 1][i >> 1], hipEventDisableSystemFence);
   if (e == hipSuccess) {
     int cus = 0;
     e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
@@ -547,7 +570,7 @@ void zdl_destroy(zdl_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (auto& r : c->rank) r.release();
   c->call.release(); c->errc.release(); c->status.release();
-  c->big_list.release(); c->counters.release(); c->slab.release();
+  c->big_list.release(); c->counters.release();
   c->cx_win.release();
   c->bits.release();
   c->big_end.release();
@@ -571,10 +594,14 @@ void zdl_destroy(zdl_ctx* c) {
   c->o_p.release(); c->o_c.release(); c->o_call.release(); c->o_err.release(); c->o_first.release();
   c->o_links.release();
   if (c->h_meta) (void)hipHostFree(c->h_meta);
+  if (c->h_map) (void)hipHostFree(c->h_map);
   if (c->h_links) (void)hipHostFree(c->h_links);
   c->mi_p.release(); c->mi_c.release(); c->mi_call.release(); c->mi_err.release();
   for (auto& ev : c->ev)
     if (ev) (void)hipEventDestroy(ev);
+  for (auto& row : c->lk_ev)
+    for (auto& ev : row)
+      if (ev) (void)hipEventDestroy(ev);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -585,7 +612,7 @@ void* zdl_stream(zdl_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
 int zdl_set_ranks(zdl_ctx* c, int dict, const int32_t* rank, uint32_t n) {
   if (!c || dict < 0 || dict > 2) return fail(c, ZDL_EINVAL, "bad dictionary");
-  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, enter(c));
   c->host_rank[dict].assign(rank, rank + n);
   if (n == 0) {
     c->nrank[dict] = 0;
@@ -611,15 +638,13 @@ int zdl_set_window(zdl_ctx* c, int64_t end_ts_ms, int64_t lookback_ms) {
 }
 
 // Default pipeline: k_link streams every trace of <= WSMALL spans, k_link_full re-runs
-// the windows it queued, k_reduce sums the dense per-workgroup tables, k_big takes the
-// traces it listed as longer than WSMALL.
+// the windows it queued, k_big takes the traces k_plan_bits listed as longer than WSMALL.
 static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans, const uint64_t* off,
                           uint64_t n_traces) {
   const size_t SS = (size_t)c->S * c->S;
   const int dense = SS <= (size_t)WDENSE_MAX;
   const int grid = c->grid, lgrid = c->cus * lk::wgs_per_cu;  // k_link: two 16-wave workgroups per CU
   HIP_TRY(c, c->big_list.ensure(n_traces));
-  if (dense) HIP_TRY(c, c->slab.ensure((size_t)lgrid * SS));  // one row per k_link workgroup
   HIP_TRY(c, c->cx_win.ensure(2 * std::min<uint64_t>(n_traces, n_spans)));
   const size_t words = (size_t)(n_spans >> 6) + 8;  // k_link reads up to 5 words past the last block
   HIP_TRY(c, c->bits.ensure(words));
@@ -639,7 +664,6 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   A.win_hi = c->win_hi;
   A.call = c->call.p;
   A.err = c->errc.p;
-  A.slab = c->slab.p;
   A.big_list = c->big_list.p;
   const uint32_t ep = c->epoch & 1u;
   A.big_count = c->counters.p + ep;
@@ -672,12 +696,6 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   HIP_TRY(c, hipLaunchKernel(k_link_full_fn(dense, c->window), dim3(grid), dim3(WPB * 64), kargs,
                              wave_block_bytes(c->window), c->stream));
   ev_record(c, 2);
-  if (dense) {
-    const uint32_t rows = (uint32_t)lgrid;
-    hipLaunchKernelGGL(k_reduce, dim3((unsigned)((SS + 255) / 256), (unsigned)((rows + REDUCE_ROWS - 1) / REDUCE_ROWS)),
-                       dim3(256), 0, c->stream, c->slab.p, rows, (uint32_t)SS, c->call.p, c->errc.p);
-    HIP_TRY(c, hipGetLastError());
-  }
   ev_record(c, 3);
   HIP_TRY(c, c->b_id.ensure(n_spans));
   HIP_TRY(c, c->b_pid.ensure(n_spans));
@@ -705,7 +723,6 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   HIP_TRY(c, hipGetLastError());
   ev_record(c, 4);
   ++c->epoch;  // k_link_full and k_big zeroed the other counter slots
-  c->times.n_tiles = 0;
   c->times.grid = (uint32_t)grid;
   return ZDL_OK;
 }
@@ -719,23 +736,17 @@ int zdl_put_spans_device(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans,
     return fail(c, ZDL_EINVAL, "missing column");
   if (c->window && !col->timestamp) return fail(c, ZDL_EINVAL, "window set but no timestamp column");
   if (n_traces >= 0xffffffffull || n_spans >= (1ull << 40)) return fail(c, ZDL_EINVAL, "input too large");
-  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, enter(c));
   return put_spans_link(c, col, n_spans, off, n_traces);
 }
 
 int zdl_sync(zdl_ctx* c) {
   if (!c) return ZDL_EINVAL;
-  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, enter(c));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   uint32_t st = 0;
   HIP_TRY(c, hipMemcpy(&st, c->status.p, 4, hipMemcpyDeviceToHost));
-  if (c->flags & ZDL_FLAG_TIMING) {
-    c->times.plan_ms = ev_ms(c, 0, 1);
-    c->times.tiles_ms = ev_ms(c, 1, 7);
-    c->times.full_ms = ev_ms(c, 7, 2);
-    c->times.reduce_ms = ev_ms(c, 2, 3);
-    c->times.big_ms = ev_ms(c, 3, 4);
-  }
+  put_times(c);
   return status_code(c, st);
 }
 
@@ -747,7 +758,7 @@ int zdl_put_spans(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans, const 
   for (uint64_t t = 0; t < n_traces; ++t)
     if (off[t + 1] < off[t]) return fail(c, ZDL_EINVAL, "trace offsets are not non-decreasing");
   if (n_spans == 0) return ZDL_OK;
-  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, enter(c));
   HIP_TRY(c, c->h_id.ensure(n_spans));
   HIP_TRY(c, c->h_pid.ensure(n_spans));
   HIP_TRY(c, c->h_lsvc.ensure(n_spans));
@@ -787,7 +798,7 @@ int zdl_put_spans(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans, const 
 
 int zdl_reset(zdl_ctx* c) {
   if (!c) return ZDL_EINVAL;
-  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, enter(c));
   const size_t SS = (size_t)c->S * c->S;
   hipLaunchKernelGGL(k_zero_tables, dim3((unsigned)((SS + 255) / 256)), dim3(256), 0, c->stream, c->call.p,
                      c->errc.p, (uint64_t)SS, c->status.p);
@@ -822,57 +833,70 @@ static void sort_output(zdl_ctx* c, size_t n) {
 int zdl_link(zdl_ctx* c, int order, zdl_links* out) {
   if (!c || !out) return ZDL_EINVAL;
   if (order != ZDL_ORDER_SORTED) return fail(c, ZDL_EINVAL, "zdl_link supports ZDL_ORDER_SORTED");
-  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, enter(c));
   const uint64_t SS = (uint64_t)c->S * c->S;
   const bool ordered = SS <= (uint64_t)COMPACT_WG * 8;
-  HIP_TRY(c, c->o_links.ensure(SS));
   ev_record(c, 5);
-  // the record count lands next to the status word: status[0] status, status[2..3] count
-  unsigned long long* cnt = reinterpret_cast<unsigned long long*>(c->status.p + 2);
+  size_t n = 0;
+  const ZLink* recs = nullptr;
   if (ordered) {
+    // one trip: the kernel writes status, count and records into mapped pinned memory
+    if (!c->h_map) {
+      HIP_TRY(c, hipHostMalloc((void**)&c->h_map, 16 + (size_t)COMPACT_WG * 8 * sizeof(ZLink),
+                               hipHostMallocMapped | hipHostMallocCoherent));
+    }
+    unsigned long long* dmap = nullptr;
+    HIP_TRY(c, hipHostGetDevicePointer((void**)&dmap, c->h_map, 0));
     hipLaunchKernelGGL(k_compact_ordered, dim3(1), dim3(COMPACT_WG), 0, c->stream, c->call.p, c->errc.p,
-                       (uint32_t)SS, c->S, cnt, c->o_links.p);
+                       (uint32_t)SS, c->S, c->status.p, dmap);
+    HIP_TRY(c, hipGetLastError());
+    ev_record(c, 6);
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    put_times(c);
+    c->times.compact_ms = ev_ms(c, 5, 6);
+    const int rc = status_code(c, (uint32_t)c->h_map[0]);
+    if (rc != ZDL_OK) return rc;
+    n = (size_t)c->h_map[1];
+    recs = reinterpret_cast<const ZLink*>(c->h_map + 2);
   } else {
+    // the record count lands next to the status word: status[0] status, status[2..3] count
+    unsigned long long* cnt = reinterpret_cast<unsigned long long*>(c->status.p + 2);
+    HIP_TRY(c, c->o_links.ensure(SS));
     HIP_TRY(c, hipMemsetAsync(cnt, 0, 8, c->stream));
     hipLaunchKernelGGL(k_compact, dim3((unsigned)((SS + 255) / 256)), dim3(256), 0, c->stream, c->call.p, c->errc.p,
                        SS, c->S, cnt, c->o_links.p);
-  }
-  HIP_TRY(c, hipGetLastError());
-  ev_record(c, 6);
-  // one round trip for the count and the status word, one for the records
-  HIP_TRY(c, hipMemcpyAsync(c->h_meta, c->status.p, 16, hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(c, hipStreamSynchronize(c->stream));
-  if (c->flags & ZDL_FLAG_TIMING) {
-    c->times.plan_ms = ev_ms(c, 0, 1);
-    c->times.tiles_ms = ev_ms(c, 1, 7);
-    c->times.full_ms = ev_ms(c, 7, 2);
-    c->times.reduce_ms = ev_ms(c, 2, 3);
-    c->times.big_ms = ev_ms(c, 3, 4);
-    c->times.compact_ms = ev_ms(c, 5, 6);
-  }
-  const int rc = status_code(c, (uint32_t)c->h_meta[0]);
-  if (rc != ZDL_OK) return rc;
-  const size_t n = (size_t)c->h_meta[1];
-  if (n > c->h_links_cap) {
-    if (c->h_links) (void)hipHostFree(c->h_links);
-    c->h_links = nullptr;
-    c->h_links_cap = 0;
-    HIP_TRY(c, hipHostMalloc((void**)&c->h_links, n * sizeof(ZLink), hipHostMallocDefault));
-    c->h_links_cap = n;
-  }
-  if (n) {
-    HIP_TRY(c, hipMemcpyAsync(c->h_links, c->o_links.p, n * sizeof(ZLink), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipGetLastError());
+    ev_record(c, 6);
+    // one round trip for the count and the status word, one for the records
+    HIP_TRY(c, hipMemcpyAsync(c->h_meta, c->status.p, 16, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
+    put_times(c);
+    c->times.compact_ms = ev_ms(c, 5, 6);
+    const int rc = status_code(c, (uint32_t)c->h_meta[0]);
+    if (rc != ZDL_OK) return rc;
+    n = (size_t)c->h_meta[1];
+    if (n > c->h_links_cap) {
+      if (c->h_links) (void)hipHostFree(c->h_links);
+      c->h_links = nullptr;
+      c->h_links_cap = 0;
+      HIP_TRY(c, hipHostMalloc((void**)&c->h_links, n * sizeof(ZLink), hipHostMallocDefault));
+      c->h_links_cap = n;
+    }
+    if (n) {
+      HIP_TRY(c, hipMemcpyAsync(c->h_links, c->o_links.p, n * sizeof(ZLink), hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(c, hipStreamSynchronize(c->stream));
+    }
+    recs = c->h_links;
   }
   c->out_p.resize(n);
   c->out_c.resize(n);
   c->out_call.resize(n);
   c->out_err.resize(n);
   for (size_t i = 0; i < n; ++i) {
-    c->out_p[i] = c->h_links[i].parent;
-    c->out_c[i] = c->h_links[i].child;
-    c->out_call[i] = c->h_links[i].call;
-    c->out_err[i] = c->h_links[i].err;
+    c->out_p[i] = recs[i].parent;
+    c->out_c[i] = recs[i].child;
+    c->out_call[i] = recs[i].call;
+    c->out_err[i] = recs[i].err;
   }
   // cell order is (parent id, child id) order; names order needs the service rank table
   if (!ordered || c->nrank[0] != 0) sort_output(c, n);
@@ -887,7 +911,7 @@ int zdl_link(zdl_ctx* c, int order, zdl_links* out) {
 int zdl_merge_links(zdl_ctx* c, const int32_t* parent, const int32_t* child, const int64_t* call_count,
                     const int64_t* error_count, uint64_t n, zdl_links* out) {
   if (!c || !out) return ZDL_EINVAL;
-  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, enter(c));
   const uint64_t SS = (uint64_t)c->S * c->S;
   HIP_TRY(c, c->m_call.ensure(SS));
   HIP_TRY(c, c->m_err.ensure(SS));
@@ -962,7 +986,7 @@ int zdl_add_links(zdl_ctx* c, const int32_t* parent, const int32_t* child, const
                   const int64_t* error_count, uint64_t n) {
   if (!c) return ZDL_EINVAL;
   if (n == 0) return ZDL_OK;
-  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, enter(c));
   const uint64_t SS = (uint64_t)c->S * c->S;
   HIP_TRY(c, c->m_first.ensure(SS));
   HIP_TRY(c, c->mi_p.ensure(n));
@@ -982,7 +1006,7 @@ int zdl_add_links(zdl_ctx* c, const int32_t* parent, const int32_t* child, const
 
 int zdl_table_export(zdl_ctx* c, void* dev_call, void* dev_err) {
   if (!c || !dev_call || !dev_err) return ZDL_EINVAL;
-  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, enter(c));
   const size_t bytes = (size_t)c->S * c->S * 8;
   HIP_TRY(c, hipMemcpyAsync(dev_call, c->call.p, bytes, hipMemcpyDeviceToDevice, c->stream));
   HIP_TRY(c, hipMemcpyAsync(dev_err, c->errc.p, bytes, hipMemcpyDeviceToDevice, c->stream));
@@ -991,7 +1015,7 @@ int zdl_table_export(zdl_ctx* c, void* dev_call, void* dev_err) {
 
 int zdl_table_import(zdl_ctx* c, const void* dev_call, const void* dev_err) {
   if (!c || !dev_call || !dev_err) return ZDL_EINVAL;
-  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, enter(c));
   const size_t bytes = (size_t)c->S * c->S * 8;
   HIP_TRY(c, hipMemcpyAsync(c->call.p, dev_call, bytes, hipMemcpyDeviceToDevice, c->stream));
   HIP_TRY(c, hipMemcpyAsync(c->errc.p, dev_err, bytes, hipMemcpyDeviceToDevice, c->stream));
@@ -1000,6 +1024,21 @@ int zdl_table_import(zdl_ctx* c, const void* dev_call, const void* dev_err) {
 
 int zdl_get_kernel_times(zdl_ctx* c, zdl_kernel_times* out) {
   if (!c || !out) return ZDL_EINVAL;
+  if ((c->flags & ZDL_FLAG_TIMING) && c->lk_n) {  // mean k_link time of the last <= 64 puts
+    HIP_TRY(c, enter(c));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    const uint32_t k = std::min<uint32_t>(c->lk_n, zdl_ctx::LK_RING);
+    double sum = 0;
+    for (uint32_t j = 0; j < k; ++j) {
+      const uint32_t i = (c->lk_n - 1 - j) % zdl_ctx::LK_RING;
+      float ms = 0.f;
+      HIP_TRY(c, hipEventElapsedTime(&ms, c->lk_ev[0][i], c->lk_ev[1][i]));
+      sum += ms;
+    }
+    c->times.tiles_ms = (float)(sum / k);
+    c->times.n_tiles = k;  // the puts averaged
+    c->lk_n = 0;
+  }
   *out = c->times;
   return ZDL_OK;
 }
