@@ -28,7 +28,7 @@ sys.path.insert(0, ROOT)
 METRIC = "spans/sec linked to DependencyLinks at 1/2/4/8 MI355X; % of HBM roofline"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BYTES_PER_SPAN = 36            # id 8 + parent_id 8 + 4 x i32 dictionary ids + port_flags 4 (k_link)
-BYTES_PER_TRACE = 8            # CSR offset (k_plan_bits)
+BYTES_PER_TRACE = 8            # CSR offset (k_link plans its windows from them)
 
 
 def log(*a):
@@ -161,8 +161,9 @@ def main():
 
     if rank == 0:
         ms_step = elapsed / args.steps * 1e3
-        bytes_launch = BYTES_PER_SPAN * cols.n_spans  # what k_link must read: every span once
-        bytes_path = bytes_launch + BYTES_PER_TRACE * (cols.n_traces + 1)
+        # what k_link must read: every span once and every trace offset once
+        bytes_launch = BYTES_PER_SPAN * cols.n_spans + BYTES_PER_TRACE * (cols.n_traces + 1)
+        bytes_path = bytes_launch
         achieved = bytes_launch / (tiles * 1e-3) / 1e9
         traffic = None
         pmc = os.path.join(ROOT, "profiles", "pmc_k_link.json")

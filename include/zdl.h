@@ -109,7 +109,7 @@ typedef struct zdl_links {
 } zdl_links;
 
 typedef struct zdl_kernel_times {
-  float plan_ms;     /* memsets + k_plan_bits */
+  float plan_ms;     /* unused (0): k_link plans its windows from the offsets itself */
   float tiles_ms;    /* k_link: every trace of <= 64 spans */
   float big_ms;      /* k_big: traces > 64 spans */
   float reduce_ms;   /* unused (k_link adds its tables itself): the gap between k_link_full and k_big */

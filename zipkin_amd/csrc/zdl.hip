@@ -1,10 +1,9 @@
 // zdl.hip — MI355X (gfx950) kernels and the C ABI of libzdl.so.
 //
 // Pipeline for one zdl_put_spans over CSR-grouped traces:
-//   k_plan_bits  one pass over the trace offsets: trace-start bitmap (1 bit per span),
-//                the traces longer than WSMALL and their ends
 //   k_link       persistent waves, each streams a contiguous chunk of traces: windows of
-//                whole traces <= 64 spans are linked in registers + a small LDS hash;
+//                whole traces <= 64 spans, planned from the trace offsets, are linked in
+//                registers + a small LDS hash; traces longer than WSMALL are listed;
 //                (parent, child) counts accumulate in the workgroup's LDS table, added
 //                to the S x S table by atomics when the workgroup ends
 //   k_link_full  the windows k_link queued (fragments / duplicate ids): full
@@ -57,16 +56,14 @@ struct Args {
   int64_t win_lo, win_hi;
   unsigned long long* call;
   unsigned long long* err;
-  const uint32_t* big_list;
-  const uint32_t* big_count;
+  uint32_t* big_list;   // k_link -> k_big: the traces longer than WSMALL
+  uint32_t* big_count;
   uint32_t* status;
   uint32_t small_max;    // traces longer than this are k_big's
   uint32_t* cx_count;
   uint32_t* cx_count_next;   // the next put's counters (two slots alternate by put):
   uint32_t* big_count_next;  // zeroed by this put's last kernels, so no memset is needed
   unsigned long long* prof;  // ZDL_PROF=1: k_link phase cycles (12 counters)
-  const unsigned long long* bits;  // k_plan_bits -> k_link: trace-start bitmap
-  const uint64_t* big_end;         // k_plan_bits -> k_link: end of the big trace starting in block b
   uint64_t* cx_win;      // k_link -> k_link_full: (base | P << 48, starts mask) per window
   uint32_t skip;         // timing-only ablation of k_link (ZDL_SKIP): 32 stream only, 64 fields,
                          // 128 +hash, 256 +parents, 512 +jumping, 2048 no table adds, 4096 cache-resident
@@ -101,7 +98,7 @@ __global__ void __launch_bounds__(BIG_WG) k_big(Args A) {
   for (uint32_t bi = blockIdx.x; bi < nbig; bi += gridDim.x) {
     const uint32_t t = A.big_list[bi];
     const uint64_t b = A.off[t];
-    if (A.off[t + 1] < b || A.off[t + 1] > A.n_spans) continue;  // k_plan_bits flagged it
+    if (A.off[t + 1] < b || A.off[t + 1] > A.n_spans) continue;  // k_link flagged it
     const int n = (int)(A.off[t + 1] - b);
     View v;
     v.id = A.b_id + b;
@@ -382,11 +379,8 @@ struct zdl_ctx {
   DevBuf<uint32_t> big_list, counters;  // counters: big[2], cx[2], alternating by put
   uint32_t epoch = 0;
   DevBuf<uint64_t> cx_win;
-  DevBuf<unsigned long long> bits;
-  DevBuf<uint64_t> big_end;
   DevBuf<unsigned long long> prof;
   int prof_on = 0;
-  int check = 0;  // ZDL_CHECK=1: verify the trace-start bitmap on the device
   DevBuf<uint64_t> b_id, b_pid;
   DevBuf<int32_t> b_lsvc, b_rsvc, b_ip4, b_ip6, b_parent;
   DevBuf<uint32_t> b_pf, b_perm;
@@ -545,8 +539,6 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
                                 (int)wave_block_bytes(w));
     }
   if (e == hipSuccess) {
-    const char* ce = getenv("ZDL_CHECK");
-    c->check = ce && ce[0] == '1';
     const char* pe = getenv("ZDL_PROF");
     c->prof_on = pe && pe[0] == '1';
     if (c->prof_on) {
@@ -572,8 +564,6 @@ void zdl_destroy(zdl_ctx* c) {
   c->call.release(); c->errc.release(); c->status.release();
   c->big_list.release(); c->counters.release();
   c->cx_win.release();
-  c->bits.release();
-  c->big_end.release();
   if (c->prof_on && c->prof.p) {
     unsigned long long h[12] = {};
     if (hipMemcpy(h, c->prof.p, sizeof h, hipMemcpyDeviceToHost) == hipSuccess) {
@@ -638,7 +628,7 @@ int zdl_set_window(zdl_ctx* c, int64_t end_ts_ms, int64_t lookback_ms) {
 }
 
 // Default pipeline: k_link streams every trace of <= WSMALL spans, k_link_full re-runs
-// the windows it queued, k_big takes the traces k_plan_bits listed as longer than WSMALL.
+// the windows it queued, k_big takes the traces k_link listed as longer than WSMALL.
 static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans, const uint64_t* off,
                           uint64_t n_traces) {
   const size_t SS = (size_t)c->S * c->S;
@@ -646,9 +636,6 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   const int grid = c->grid, lgrid = c->cus * lk::wgs_per_cu;  // k_link: two 16-wave workgroups per CU
   HIP_TRY(c, c->big_list.ensure(n_traces));
   HIP_TRY(c, c->cx_win.ensure(2 * std::min<uint64_t>(n_traces, n_spans)));
-  const size_t words = (size_t)(n_spans >> 6) + 8;  // k_link reads up to 5 words past the last block
-  HIP_TRY(c, c->bits.ensure(words));
-  HIP_TRY(c, c->big_end.ensure(words));
   Args A{};
   A.c = Cols{col->id, col->parent_id, col->local_svc, col->remote_svc, col->local_ip4, col->local_ip6,
              col->port_flags, col->timestamp};
@@ -675,23 +662,11 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   A.cx_win = c->cx_win.p;
   A.skip = c->skip;
   A.prof = c->prof.p;
-  A.bits = c->bits.p;
-  A.big_end = c->big_end.p;
-  const unsigned long long* bits_arg = c->bits.p;
   void* kargs[] = {&A};
-  void* lkargs[] = {&A, &bits_arg};
   ev_record(c, 0);
-  hipLaunchKernelGGL(k_plan_bits, dim3((unsigned)((n_traces + 255) / 256)), dim3(256), 0, c->stream, off, n_traces,
-                     n_spans, c->bits.p, (uint64_t)words, c->big_end.p, c->big_list.p, c->counters.p + ep, c->status.p);
-  HIP_TRY(c, hipGetLastError());
   ev_record(c, 1);
-  HIP_TRY(c, hipLaunchKernel(k_link_fn(dense, c->window, c->prof_on ? 1 : (c->skip ? 2 : 0)), dim3(lgrid), dim3(lk::waves(c->window) * 64), lkargs,
-                             link_block_bytes(c->window), c->stream));
-  if (c->check) {  // after k_link: checks what k_link read
-    const uint64_t nthr = std::max<uint64_t>(n_traces, words);
-    hipLaunchKernelGGL(k_check_bits, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, c->stream, off, n_traces,
-                       n_spans, c->bits.p, c->status.p);
-  }
+  HIP_TRY(c, hipLaunchKernel(k_link_fn(dense, c->window, c->prof_on ? 1 : (c->skip ? 2 : 0)), dim3(lgrid),
+                             dim3(lk::waves(c->window) * 64), kargs, link_block_bytes(c->window), c->stream));
   ev_record(c, 7);
   HIP_TRY(c, hipLaunchKernel(k_link_full_fn(dense, c->window), dim3(grid), dim3(WPB * 64), kargs,
                              wave_block_bytes(c->window), c->stream));
