@@ -1,9 +1,9 @@
 """Benchmark: spans/sec linked to DependencyLinks on MI355X (BASELINE.json metric).
 
 One step = one pass of the hot path over one batch already resident in HBM:
-reset the S x S counts, zdl_put_spans_device (k_plan_bits, k_link, k_link_full,
-k_reduce, k_big), for N > 1 one RCCL all-reduce of the count tables, then zdl_link
-(ordered compaction, one D2H of the records) -> the DependencyLink list.
+reset the S x S counts, zdl_put_spans_device (k_link, k_link_full, k_big), for N > 1
+one RCCL all-reduce of the count tables, then zdl_link (ordered compaction into mapped
+pinned memory, one sync) -> the DependencyLink list.
 
 N = 1 runs C2 (10M spans / 1M traces / 50 services). N > 1 is weak scaling:
 every rank links its own C2-sized shard of traces picked by
