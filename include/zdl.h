@@ -111,11 +111,11 @@ typedef struct zdl_links {
 typedef struct zdl_kernel_times {
   float plan_ms;     /* unused (0): k_link plans its windows from the offsets itself */
   float tiles_ms;    /* k_link: every trace of <= 64 spans */
-  float big_ms;      /* k_big: traces > 64 spans */
-  float reduce_ms;   /* unused (k_link adds its tables itself): the gap between k_link_full and k_big */
+  float big_ms;      /* k_tail: queued windows, traces > 64 spans, ordered compaction */
+  float reduce_ms;   /* unused (0) */
   float compact_ms;  /* k_compact (zdl_link) */
   uint32_t n_tiles, n_big, grid;  /* n_tiles: puts averaged into tiles_ms (ZDL_FLAG_TIMING) */
-  float full_ms;     /* k_link_full: windows with fragments / duplicate ids */
+  float full_ms;     /* unused (0): k_tail runs the queued windows */
 } zdl_kernel_times;
 
 /* Context lifecycle. zdl_create returns NULL on failure (zdl_create_error() says why). */

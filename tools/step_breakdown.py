@@ -50,6 +50,8 @@ def main():
             "put": lambda: put(ctx),
             "reset+put": lambda: (ctx.reset(), put(ctx)),
             "link": lambda: ctx.link(),
+            "sync": lambda: ctx.sync(),
+            "raw_link": lambda: ctx._L.zdl_link(ctx.h, N.ZDL_ORDER_SORTED, N.C.byref(N.Links())),
             "step": lambda: (ctx.reset(), put(ctx), ctx.link()),
         }
         for name, fn in parts.items():

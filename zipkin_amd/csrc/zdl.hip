@@ -6,10 +6,13 @@
 //                registers + a small LDS hash; traces longer than WSMALL are listed;
 //                (parent, child) counts accumulate in the workgroup's LDS table, added
 //                to the S x S table by atomics when the workgroup ends
-//   k_link_full  the windows k_link queued (fragments / duplicate ids): full
-//                Trace.merge + SpanNode.Builder emulation, one wave per window
-//   k_big        one workgroup per trace longer than WSMALL, HBM scratch, bitonic sort
-// zdl_link compacts the non-zero cells (k_compact) and sorts them by service rank.
+//   k_tail       one 1024-thread workgroup per CU: the windows k_link queued (fragments /
+//                duplicate ids: full Trace.merge + SpanNode.Builder emulation, one wave
+//                per window), then one workgroup per trace longer than WSMALL (HBM
+//                scratch, bitonic sort), then the last workgroup compacts a small table
+//                into mapped host memory
+// zdl_link reads that (or compacts the non-zero cells itself: k_compact_ordered /
+// k_compact) and sorts by service rank when ranks are set.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -28,7 +31,7 @@ constexpr int BIG_WG = 1024;        // threads per big-trace workgroup
 constexpr int HCAP = 2048;          // LDS hash slots of the (parent, child) table when S*S is large
 constexpr int HPROBE = 64;
 constexpr int WSMALL = 64;          // traces up to this many spans are k_link's
-constexpr int WPB = 8;              // waves per k_link_full workgroup
+constexpr int TAIL_WG = 1024;       // threads per k_tail workgroup (= BIG_WG)
 constexpr int WDENSE_MAX = 2560;    // S*S <= this -> dense u64 LDS cells (call | err << 32)
 constexpr int WTABLE_BYTES = 24576; // max(8 * (WDENSE_MAX + 64 dummy cells), 12 * HCAP)
 static_assert(8 * (WDENSE_MAX + 64) <= WTABLE_BYTES && 12 * HCAP <= WTABLE_BYTES, "LDS table carve");
@@ -56,15 +59,18 @@ struct Args {
   int64_t win_lo, win_hi;
   unsigned long long* call;
   unsigned long long* err;
-  uint32_t* big_list;   // k_link -> k_big: the traces longer than WSMALL
+  uint32_t* big_list;   // k_link -> k_tail: the traces longer than WSMALL
   uint32_t* big_count;
   uint32_t* status;
-  uint32_t small_max;    // traces longer than this are k_big's
+  uint32_t small_max;    // traces longer than this are k_tail's (big_traces)
   uint32_t* cx_count;
   uint32_t* cx_count_next;   // the next put's counters (two slots alternate by put):
-  uint32_t* big_count_next;  // zeroed by this put's last kernels, so no memset is needed
+  uint32_t* big_count_next;  // zeroed by this put's k_tail, so no memset is needed
+  unsigned long long* map;   // mapped pinned host buffer: k_tail's last workgroup writes the
+                             // ordered link records there (S*S <= 8192), else nullptr
+  uint32_t* done;            // k_tail workgroups finished (the last one compacts; resets it)
   unsigned long long* prof;  // ZDL_PROF=1: k_link phase cycles (12 counters)
-  uint64_t* cx_win;      // k_link -> k_link_full: (base | P << 48, starts mask) per window
+  uint64_t* cx_win;      // k_link -> k_tail: (base | P << 48, starts mask) per window
   uint32_t skip;         // timing-only ablation of k_link (ZDL_SKIP): 32 stream only, 64 fields,
                          // 128 +hash, 256 +parents, 512 +jumping, 2048 no table adds, 4096 cache-resident
   // big-trace scratch (HBM), indexed by global span index
@@ -81,19 +87,19 @@ struct Args {
   uint8_t* b_haschild;
 };
 
-#include "zdl_full.inc"  // the full per-window emulation (k_link_full's phases)
-#include "zdl_link.inc"  // k_link, k_link_full (need zdl_full.inc's helpers)
+#include "zdl_full.inc"  // the full per-window emulation (k_tail's first part)
+#include "zdl_link.inc"  // k_link, full_windows (need zdl_full.inc's helpers)
 
-// -------------------------------------------------------------------- k_big
-// One workgroup per trace longer than WSMALL; arrays live in HBM scratch at the trace's
-// global span offset. zdl_algo.h's phases, bitonic sort instead of ranks.
+// ---------------------------------------------------------- big traces (k_tail)
+// k_tail's second part: one workgroup per trace longer than WSMALL; arrays live in HBM
+// scratch at the trace's global span offset. zdl_algo.h's phases, bitonic sort instead of
+// ranks.
 __device__ __forceinline__ void big_sync() { __syncthreads(); }
 
-__global__ void __launch_bounds__(BIG_WG) k_big(Args A) {
+__device__ __forceinline__ void big_traces(const Args& A) {
   __shared__ int32_t sh_root;
   __shared__ int sh_act;
   __shared__ int64_t sh_ts_root_idx, sh_ts_min;
-  if (blockIdx.x == 0 && threadIdx.x == 0) *A.big_count_next = 0;
   const uint32_t nbig = *A.big_count;
   for (uint32_t bi = blockIdx.x; bi < nbig; bi += gridDim.x) {
     const uint32_t t = A.big_list[bi];
@@ -241,18 +247,44 @@ struct ZLink {
 // Non-zero cells -> records, in cell order (= (parent id, child id) order): one workgroup,
 // a block-wide exclusive scan of the per-thread non-zero counts. For S*S <= 1024 * 8.
 constexpr int COMPACT_WG = 1024;
-// Writes straight into the context's mapped pinned buffer: meta[0] = the status word,
-// meta[1] = the record count, then the records (the host reads them after one sync).
-__global__ void __launch_bounds__(COMPACT_WG) k_compact_ordered(const unsigned long long* __restrict__ call,
-                                                                const unsigned long long* __restrict__ err,
-                                                                uint32_t SS, uint32_t S,
-                                                                const uint32_t* __restrict__ status,
-                                                                unsigned long long* __restrict__ meta) {
-  ZLink* __restrict__ out = reinterpret_cast<ZLink*>(meta + 2);
+constexpr size_t MAP_CAP = (size_t)COMPACT_WG * 8;  // records of the mapped output
+// The mapped output, columns (lanes store consecutive 4 / 8 B: few host-bus transactions):
+// u64 meta[2] = {status word, record count}, i32 parent[MAP_CAP], i32 child[MAP_CAP],
+// i64 call[MAP_CAP], i64 err[MAP_CAP].
+constexpr size_t MAP_BYTES = 16 + MAP_CAP * 24;
+struct MapCols {
+  int32_t* parent;
+  int32_t* child;
+  int64_t* call;
+  int64_t* err;
+};
+__host__ __device__ inline MapCols map_cols(unsigned long long* meta) {
+  unsigned char* b = reinterpret_cast<unsigned char*>(meta) + 16;
+  return MapCols{reinterpret_cast<int32_t*>(b), reinterpret_cast<int32_t*>(b + 4 * MAP_CAP),
+                 reinterpret_cast<int64_t*>(b + 8 * MAP_CAP), reinterpret_cast<int64_t*>(b + 16 * MAP_CAP)};
+}
+// Writes into mapped pinned host memory: meta[0] = the status word, meta[1] = the record
+// count, then the records (the host reads them after one sync). One workgroup of
+// COMPACT_WG threads; every thread of it must call.
+__device__ __forceinline__ unsigned long long ld_agent(const unsigned long long* p) {  // device-coherent read
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void compact_ordered(const unsigned long long* __restrict__ call,
+                                                const unsigned long long* __restrict__ err, uint32_t SS,
+                                                uint32_t S, const uint32_t* __restrict__ status,
+                                                unsigned long long* __restrict__ meta) {
+  constexpr int KMAX = 8;  // cells per thread: SS <= COMPACT_WG * KMAX
+  const MapCols out = map_cols(meta);
   __shared__ uint32_t wsum[COMPACT_WG / 64 + 1];
   const uint32_t K = (SS + COMPACT_WG - 1) / COMPACT_WG, c0 = threadIdx.x * K;
+  unsigned long long cv[KMAX];
   uint32_t nz = 0;
-  for (uint32_t k = 0; k < K; ++k) nz += (c0 + k < SS && call[c0 + k] != 0) ? 1u : 0u;
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) {
+    cv[k] = (uint32_t)k < K && c0 + k < SS ? ld_agent(&call[c0 + k]) : 0ull;
+    nz += cv[k] != 0 ? 1u : 0u;
+  }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   uint32_t incl = nz;
 #pragma unroll
@@ -270,18 +302,68 @@ __global__ void __launch_bounds__(COMPACT_WG) k_compact_ordered(const unsigned l
       acc += t;
     }
     wsum[COMPACT_WG / 64] = acc;
-    meta[0] = *status;
+    meta[0] = __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     meta[1] = acc;
   }
   __syncthreads();
   uint32_t o = wsum[w] + incl - nz;
-  for (uint32_t k = 0; k < K; ++k) {
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) {
+    if (cv[k] == 0) continue;
     const uint32_t i = c0 + k;
-    if (i >= SS) break;
-    const unsigned long long n = call[i];
-    if (n == 0) continue;
-    out[o++] = ZLink{(int32_t)(i / S), (int32_t)(i % S), (int64_t)n, (int64_t)err[i]};
+    out.parent[o] = (int32_t)(i / S);
+    out.child[o] = (int32_t)(i % S);
+    out.call[o] = (int64_t)cv[k];
+    out.err[o] = (int64_t)ld_agent(&err[i]);
+    ++o;
   }
+}
+
+__global__ void __launch_bounds__(COMPACT_WG) k_compact_ordered(const unsigned long long* __restrict__ call,
+                                                                const unsigned long long* __restrict__ err,
+                                                                uint32_t SS, uint32_t S,
+                                                                const uint32_t* __restrict__ status,
+                                                                unsigned long long* __restrict__ meta) {
+  compact_ordered(call, err, SS, S, status, meta);
+}
+
+// ------------------------------------------------------------------- k_tail
+// The put's last kernel, one 1024-thread workgroup per CU: the windows k_link queued (one
+// wave each), then the traces longer than WSMALL (one workgroup each), then - when the
+// table is small enough for ordered output - the last workgroup to finish compacts the
+// table into the mapped host buffer, so zdl_link needs no kernel. Also zeroes the next
+// put's counters.
+static_assert(TAIL_WG == BIG_WG && TAIL_WG == COMPACT_WG, "k_tail runs all three parts");
+inline size_t tail_block_bytes(int window) { return WTABLE_BYTES + (TAIL_WG / 64) * wl::bytes(window); }
+
+template <int DENSE, int WINDOW>
+__global__ void __launch_bounds__(TAIL_WG, 1) k_tail(Args A) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  __shared__ bool last;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    *A.cx_count_next = 0;
+    *A.big_count_next = 0;
+  }
+  full_windows<DENSE, WINDOW, TAIL_WG / 64>(A, lds);
+  __syncthreads();
+  big_traces(A);
+  if (!A.map) return;
+  // The table and status atomics are performed at the device-coherent level; waiting for
+  // this workgroup's to complete (vmcnt) before counting it done is enough, and the last
+  // workgroup reads the cells with device-coherent loads. (Agent-scope fences here cost an
+  // L2 writeback / invalidate per workgroup: 37 us measured.)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __syncthreads();
+  if (threadIdx.x == 0) last = atomicAdd(A.done, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  compact_ordered(A.call, A.err, A.S * A.S, A.S, A.status, A.map);
+  if (threadIdx.x == 0) *A.done = 0;
+}
+
+inline const void* k_tail_fn(int dense, int window) {
+  if (dense) return window ? (const void*)k_tail<1, 1> : (const void*)k_tail<1, 0>;
+  return window ? (const void*)k_tail<0, 1> : (const void*)k_tail<0, 0>;
 }
 
 // Any S: non-zero cells -> records in arbitrary order (the host sorts them).
@@ -396,7 +478,9 @@ struct zdl_ctx {
   DevBuf<int64_t> o_call, o_err;
   DevBuf<ZLink> o_links;
   uint64_t* h_meta = nullptr;  // pinned: link count, status
-  unsigned long long* h_map = nullptr;  // mapped pinned: k_compact_ordered's status, count, records
+  unsigned long long* h_map = nullptr;  // mapped pinned: status, count, ordered records
+  unsigned long long* d_map = nullptr;  // its device address
+  bool map_fresh = false;               // h_map holds the compaction of the current table
   ZLink* h_links = nullptr;    // pinned link records
   size_t h_links_cap = 0;
   DevBuf<uint64_t> o_first;
@@ -514,8 +598,8 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
   if (e == hipSuccess) e = hipMemset(c->call.p, 0, SS * 8);
   if (e == hipSuccess) e = hipMemset(c->errc.p, 0, SS * 8);
   if (e == hipSuccess) e = hipMemset(c->status.p, 0, 16);
-  if (e == hipSuccess) e = c->counters.ensure(4);
-  if (e == hipSuccess) e = hipMemset(c->counters.p, 0, 16);
+  if (e == hipSuccess) e = c->counters.ensure(5);  // + k_tail's finished-workgroup count
+  if (e == hipSuccess) e = hipMemset(c->counters.p, 0, 20);
   if (e == hipSuccess) e = hipHostMalloc((void**)&c->h_meta, 16, hipHostMallocDefault);
   // timing-only events: no system-scope fence (cache writeback) between the kernels they bracket
   for (int i = 0; i < 8 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->ev[i], hipEventDisableSystemFence);
@@ -525,7 +609,7 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
     int cus = 0;
     e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
     c->cus = std::max(1, cus);
-    c->grid = c->cus * 2;  // k_link_full: two 512-thread workgroups per CU
+    c->grid = c->cus;  // k_tail: one 1024-thread workgroup per CU
   }
   for (int d = 0; d < 2 && e == hipSuccess; ++d)
     for (int w = 0; w < 2 && e == hipSuccess; ++w) {
@@ -535,8 +619,8 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
         e = hipFuncSetAttribute(k_link_fn(1, 0, m), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)link_block_bytes(0));
       if (e == hipSuccess)
-        e = hipFuncSetAttribute(k_link_full_fn(d, w), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)wave_block_bytes(w));
+        e = hipFuncSetAttribute(k_tail_fn(d, w), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)tail_block_bytes(w));
     }
   if (e == hipSuccess) {
     const char* pe = getenv("ZDL_PROF");
@@ -627,8 +711,17 @@ int zdl_set_window(zdl_ctx* c, int64_t end_ts_ms, int64_t lookback_ms) {
   return ZDL_OK;
 }
 
-// Default pipeline: k_link streams every trace of <= WSMALL spans, k_link_full re-runs
-// the windows it queued, k_big takes the traces k_link listed as longer than WSMALL.
+// The mapped pinned buffer of ordered link output (S*S <= COMPACT_WG * 8).
+static hipError_t ensure_map(zdl_ctx* c) {
+  if (c->h_map) return hipSuccess;
+  hipError_t e = hipHostMalloc((void**)&c->h_map, MAP_BYTES, hipHostMallocMapped | hipHostMallocCoherent);
+  if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&c->d_map, c->h_map, 0);
+  return e;
+}
+
+// Default pipeline: k_link streams every trace of <= WSMALL spans; k_tail re-runs the
+// windows it queued, takes the traces it listed as longer than WSMALL and (small tables)
+// compacts the table into the mapped buffer zdl_link reads.
 static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans, const uint64_t* off,
                           uint64_t n_traces) {
   const size_t SS = (size_t)c->S * c->S;
@@ -668,8 +761,6 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   HIP_TRY(c, hipLaunchKernel(k_link_fn(dense, c->window, c->prof_on ? 1 : (c->skip ? 2 : 0)), dim3(lgrid),
                              dim3(lk::waves(c->window) * 64), kargs, link_block_bytes(c->window), c->stream));
   ev_record(c, 7);
-  HIP_TRY(c, hipLaunchKernel(k_link_full_fn(dense, c->window), dim3(grid), dim3(WPB * 64), kargs,
-                             wave_block_bytes(c->window), c->stream));
   ev_record(c, 2);
   ev_record(c, 3);
   HIP_TRY(c, c->b_id.ensure(n_spans));
@@ -694,10 +785,15 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   A.b_parent = c->b_parent.p;
   A.b_live = c->b_live.p;
   A.b_haschild = c->b_hasc.p;
-  hipLaunchKernelGGL(k_big, dim3(256), dim3(BIG_WG), 0, c->stream, A);
-  HIP_TRY(c, hipGetLastError());
+  const bool ordered = SS <= (size_t)COMPACT_WG * 8;
+  if (ordered) HIP_TRY(c, ensure_map(c));
+  A.map = ordered && !getenv("ZDL_NOTAILMAP") ? c->d_map : nullptr;
+  A.done = c->counters.p + 4;
+  HIP_TRY(c, hipLaunchKernel(k_tail_fn(dense, c->window), dim3(grid), dim3(TAIL_WG), kargs,
+                             tail_block_bytes(c->window), c->stream));
   ev_record(c, 4);
-  ++c->epoch;  // k_link_full and k_big zeroed the other counter slots
+  ++c->epoch;  // k_tail zeroed the other counter slots
+  c->map_fresh = A.map != nullptr;
   c->times.grid = (uint32_t)grid;
   return ZDL_OK;
 }
@@ -778,6 +874,7 @@ int zdl_reset(zdl_ctx* c) {
   hipLaunchKernelGGL(k_zero_tables, dim3((unsigned)((SS + 255) / 256)), dim3(256), 0, c->stream, c->call.p,
                      c->errc.p, (uint64_t)SS, c->status.p);
   HIP_TRY(c, hipGetLastError());
+  c->map_fresh = false;
   return ZDL_OK;  // stream-ordered: no host wait
 }
 
@@ -814,17 +911,17 @@ int zdl_link(zdl_ctx* c, int order, zdl_links* out) {
   ev_record(c, 5);
   size_t n = 0;
   const ZLink* recs = nullptr;
+  c->out_p.clear();
   if (ordered) {
-    // one trip: the kernel writes status, count and records into mapped pinned memory
-    if (!c->h_map) {
-      HIP_TRY(c, hipHostMalloc((void**)&c->h_map, 16 + (size_t)COMPACT_WG * 8 * sizeof(ZLink),
-                               hipHostMallocMapped | hipHostMallocCoherent));
+    // status, count and records land in mapped pinned memory: written by the last put's
+    // k_tail, or here when the table changed since
+    HIP_TRY(c, ensure_map(c));
+    if (!c->map_fresh) {
+      hipLaunchKernelGGL(k_compact_ordered, dim3(1), dim3(COMPACT_WG), 0, c->stream, c->call.p, c->errc.p,
+                         (uint32_t)SS, c->S, c->status.p, c->d_map);
+      HIP_TRY(c, hipGetLastError());
+      c->map_fresh = true;
     }
-    unsigned long long* dmap = nullptr;
-    HIP_TRY(c, hipHostGetDevicePointer((void**)&dmap, c->h_map, 0));
-    hipLaunchKernelGGL(k_compact_ordered, dim3(1), dim3(COMPACT_WG), 0, c->stream, c->call.p, c->errc.p,
-                       (uint32_t)SS, c->S, c->status.p, dmap);
-    HIP_TRY(c, hipGetLastError());
     ev_record(c, 6);
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     put_times(c);
@@ -832,7 +929,11 @@ int zdl_link(zdl_ctx* c, int order, zdl_links* out) {
     const int rc = status_code(c, (uint32_t)c->h_map[0]);
     if (rc != ZDL_OK) return rc;
     n = (size_t)c->h_map[1];
-    recs = reinterpret_cast<const ZLink*>(c->h_map + 2);
+    const MapCols m = map_cols(c->h_map);
+    c->out_p.assign(m.parent, m.parent + n);
+    c->out_c.assign(m.child, m.child + n);
+    c->out_call.assign(m.call, m.call + n);
+    c->out_err.assign(m.err, m.err + n);
   } else {
     // the record count lands next to the status word: status[0] status, status[2..3] count
     unsigned long long* cnt = reinterpret_cast<unsigned long long*>(c->status.p + 2);
@@ -863,15 +964,17 @@ int zdl_link(zdl_ctx* c, int order, zdl_links* out) {
     }
     recs = c->h_links;
   }
-  c->out_p.resize(n);
-  c->out_c.resize(n);
-  c->out_call.resize(n);
-  c->out_err.resize(n);
-  for (size_t i = 0; i < n; ++i) {
-    c->out_p[i] = recs[i].parent;
-    c->out_c[i] = recs[i].child;
-    c->out_call[i] = recs[i].call;
-    c->out_err[i] = recs[i].err;
+  if (recs) {
+    c->out_p.resize(n);
+    c->out_c.resize(n);
+    c->out_call.resize(n);
+    c->out_err.resize(n);
+    for (size_t i = 0; i < n; ++i) {
+      c->out_p[i] = recs[i].parent;
+      c->out_c[i] = recs[i].child;
+      c->out_call[i] = recs[i].call;
+      c->out_err[i] = recs[i].err;
+    }
   }
   // cell order is (parent id, child id) order; names order needs the service rank table
   if (!ordered || c->nrank[0] != 0) sort_output(c, n);
@@ -976,6 +1079,7 @@ int zdl_add_links(zdl_ctx* c, const int32_t* parent, const int32_t* child, const
   hipLaunchKernelGGL(k_merge_accum, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, c->mi_p.p, c->mi_c.p,
                      c->mi_call.p, c->mi_err.p, n, c->S, c->call.p, c->errc.p, c->m_first.p, c->status.p);
   HIP_TRY(c, hipGetLastError());
+  c->map_fresh = false;
   return zdl_sync(c);
 }
 
@@ -994,6 +1098,7 @@ int zdl_table_import(zdl_ctx* c, const void* dev_call, const void* dev_err) {
   const size_t bytes = (size_t)c->S * c->S * 8;
   HIP_TRY(c, hipMemcpyAsync(c->call.p, dev_call, bytes, hipMemcpyDeviceToDevice, c->stream));
   HIP_TRY(c, hipMemcpyAsync(c->errc.p, dev_err, bytes, hipMemcpyDeviceToDevice, c->stream));
+  c->map_fresh = false;
   return ZDL_OK;
 }
 
