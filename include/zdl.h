@@ -81,7 +81,8 @@ extern "C" {
  * (Span.Builder coerces empty endpoints to null, Span.java:527-536).
  */
 typedef struct zdl_span_cols {
-  const uint64_t* trace_lo;   /* low 64 bits of the trace id (sharding/grouping; not read by zdl_put_spans) */
+  const uint64_t* trace_lo;   /* low 64 bits of the trace id: read only to group ungrouped input
+                                 (trace_offsets == NULL), like InMemoryStorage.getDependencies */
   const uint64_t* id;         /* span id, != 0 */
   const uint64_t* parent_id;  /* 0 = null; parent_id == id is treated as null (Span.java:611-617) */
   const int32_t*  local_svc;  /* service dictionary id, -1 = null */
@@ -90,6 +91,8 @@ typedef struct zdl_span_cols {
   const int32_t*  local_ip6;  /* ipv6 dictionary id, -1 = null */
   const uint32_t* port_flags; /* see ZDL_PF_* */
   const int64_t*  timestamp;  /* epoch micros, 0 = absent; read only when a window is set */
+  const uint32_t* ord;        /* optional storage order within a trace (ungrouped input only);
+                                 NULL = the input order is the storage order */
 } zdl_span_cols;
 
 typedef struct zdl_config {
@@ -137,7 +140,11 @@ int zdl_set_window(zdl_ctx* ctx, int64_t end_ts_ms, int64_t lookback_ms);
 /* putTrace over n_traces CSR-grouped traces from HOST buffers: trace t is spans
  * [trace_offsets[t], trace_offsets[t+1]) in storage order; trace_offsets has n_traces+1
  * entries, starts at 0 and ends at n_spans. Synchronous. Counts accumulate in the
- * context across calls. On ZDL_EREF_NPE the counts are unspecified until zdl_reset. */
+ * context across calls. On ZDL_EREF_NPE the counts are unspecified until zdl_reset.
+ * trace_offsets == NULL: the spans are ungrouped; they are grouped on the device by
+ * trace_lo (stable in `ord`, else input order; n_traces is ignored, n_spans < 2^32),
+ * as InMemoryStorage.getDependencies groups by lowTraceId (InMemoryStorage.java:323-332,
+ * 448-467). */
 int zdl_put_spans(zdl_ctx* ctx, const zdl_span_cols* cols, uint64_t n_spans,
                   const uint64_t* trace_offsets, uint64_t n_traces);
 

@@ -190,3 +190,50 @@ def test_bad_service_id_is_einval():
     with pytest.raises(N.ZdlError):
         ctx.put_spans(cols)
     ctx.close()
+
+
+def _sorted_links(ctx):
+    p, c, n, e = ctx.link()
+    return sorted(zip(p.tolist(), c.tolist(), n.tolist(), e.tolist()))
+
+
+def _interleave_keep_order(owner, rng):
+    # draw a random sequence of trace labels with each trace's multiplicity, then give the
+    # k-th occurrence of trace t the k-th span of t
+    labels = rng.permutation(owner)
+    first = np.zeros(owner.max() + 2, np.int64)
+    np.add.at(first, owner + 1, 1)
+    start = np.cumsum(first)[:-1]
+    k = np.zeros(len(owner), np.int64)
+    seen = np.zeros(owner.max() + 1, np.int64)
+    for i, t in enumerate(labels):
+        k[i] = start[t] + seen[t]
+        seen[t] += 1
+    return k
+
+
+def _take(cols, idx):
+    from zipkin_amd.columnar import Columns
+    f = ("trace_lo", "id", "parent_id", "local_svc", "remote_svc", "local_ip4", "local_ip6", "port_flags",
+         "timestamp")
+    return Columns(*(np.ascontiguousarray(getattr(cols, n)[idx]) for n in f), cols.offsets)
+
+
+@pytest.mark.parametrize("use_ord", [False, True])
+def test_ungrouped_input_grouped_on_device(use_ord):
+    """trace_offsets == NULL: the device groups by trace_lo (InMemoryStorage.java:448-467)."""
+    w = synth.C2.scaled(20_000)
+    cols = synth.generate(w)
+    rng = np.random.default_rng(7)
+    ctx = N.Context(w.total_services)
+    ctx.put_spans(cols)
+    exp = _sorted_links(ctx)
+    ctx.reset()
+    if use_ord:  # any span order; ord = the position within the trace's storage order
+        idx = rng.permutation(cols.n_spans)
+        ctx.put_spans_ungrouped(_take(cols, idx), ord=idx.astype(np.uint32))
+    else:  # traces interleaved, each trace's spans still in storage order
+        ctx.put_spans_ungrouped(_take(cols, _interleave_keep_order(
+            np.repeat(np.arange(cols.n_traces), np.diff(cols.offsets.astype(np.int64))), rng)))
+    assert _sorted_links(ctx) == exp
+    ctx.close()

@@ -36,7 +36,7 @@ EXPORTS = (
 class SpanCols(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in (
         "trace_lo", "id", "parent_id", "local_svc", "remote_svc", "local_ip4", "local_ip6",
-        "port_flags", "timestamp")]
+        "port_flags", "timestamp", "ord")]
 
 
 class Config(C.Structure):
@@ -162,9 +162,19 @@ class Context:
                       _ptr(cols.local_ip4), _ptr(cols.local_ip6), _ptr(cols.port_flags), _ptr(cols.timestamp))
         self.check(self._L.zdl_put_spans(self.h, C.byref(sc), cols.n_spans, _ptr(cols.offsets), cols.n_traces))
 
+    def put_spans_ungrouped(self, cols, ord=None) -> None:
+        """Host columns in any trace order (cols.trace_lo read, cols.offsets ignored): the
+        device groups them by trace_lo, stable in `ord` (u32 storage order) or input order."""
+        o = None if ord is None else np.ascontiguousarray(ord, np.uint32)
+        sc = SpanCols(_ptr(cols.trace_lo), _ptr(cols.id), _ptr(cols.parent_id), _ptr(cols.local_svc),
+                      _ptr(cols.remote_svc), _ptr(cols.local_ip4), _ptr(cols.local_ip6), _ptr(cols.port_flags),
+                      _ptr(cols.timestamp), _ptr(o) if o is not None else None)
+        self.check(self._L.zdl_put_spans(self.h, C.byref(sc), cols.n_spans, None, 0))
+
     def put_spans_device(self, ptrs: dict, n_spans: int, offsets_ptr: int, n_traces: int) -> None:
-        sc = SpanCols(None, *(ptrs.get(k) for k in ("id", "parent_id", "local_svc", "remote_svc", "local_ip4",
-                                                    "local_ip6", "port_flags", "timestamp")))
+        sc = SpanCols(ptrs.get("trace_lo"), *(ptrs.get(k) for k in ("id", "parent_id", "local_svc", "remote_svc",
+                                                                   "local_ip4", "local_ip6", "port_flags",
+                                                                   "timestamp", "ord")))
         self.check(self._L.zdl_put_spans_device(self.h, C.byref(sc), n_spans, offsets_ptr, n_traces))
 
     def sync(self):

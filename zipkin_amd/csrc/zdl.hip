@@ -15,6 +15,8 @@
 // k_compact) and sorts by service rank when ranks are set.
 #include <hip/hip_runtime.h>
 
+#include "zdl_group.h"
+
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -49,6 +51,7 @@ struct Cols {
 
 struct Args {
   Cols c;
+  const uint64_t* n_traces_dev;  // device-side trace count (grouped on the device), else null
   const uint64_t* off;
   uint64_t n_traces;
   uint64_t n_spans;
@@ -470,8 +473,15 @@ struct zdl_ctx {
   // host-API staging
   DevBuf<uint64_t> h_id, h_pid, h_off;
   DevBuf<int32_t> h_lsvc, h_rsvc, h_ip4, h_ip6;
-  DevBuf<uint32_t> h_pf;
+  DevBuf<uint32_t> h_pf, h_ord;
   DevBuf<int64_t> h_ts;
+  DevBuf<uint64_t> h_lo;
+  // ungrouped input: zdl_group's sort + the columns in grouped order
+  GroupWork grp;
+  DevBuf<uint64_t> g_id, g_pid;
+  DevBuf<int32_t> g_lsvc, g_rsvc, g_ip4, g_ip6;
+  DevBuf<uint32_t> g_pf;
+  DevBuf<int64_t> g_ts;
   // link output
   DevBuf<unsigned long long> count, m_call, m_err, m_first;
   DevBuf<int32_t> o_p, o_c;
@@ -664,6 +674,9 @@ void zdl_destroy(zdl_ctx* c) {
   c->b_hasc.release();
   c->h_id.release(); c->h_pid.release(); c->h_off.release(); c->h_lsvc.release(); c->h_rsvc.release();
   c->h_ip4.release(); c->h_ip6.release(); c->h_pf.release(); c->h_ts.release();
+  c->h_lo.release(); c->h_ord.release(); c->grp.release();
+  c->g_id.release(); c->g_pid.release(); c->g_lsvc.release(); c->g_rsvc.release(); c->g_ip4.release();
+  c->g_ip6.release(); c->g_pf.release(); c->g_ts.release();
   c->count.release(); c->m_call.release(); c->m_err.release(); c->m_first.release();
   c->o_p.release(); c->o_c.release(); c->o_call.release(); c->o_err.release(); c->o_first.release();
   c->o_links.release();
@@ -711,6 +724,24 @@ int zdl_set_window(zdl_ctx* c, int64_t end_ts_ms, int64_t lookback_ms) {
   return ZDL_OK;
 }
 
+// Ungrouped input: the columns in grouped order (perm = zdl_group's sorted positions).
+__global__ void k_gather(Cols in, const uint32_t* __restrict__ perm, uint64_t n, uint64_t* __restrict__ id,
+                         uint64_t* __restrict__ pid, int32_t* __restrict__ lsvc, int32_t* __restrict__ rsvc,
+                         int32_t* __restrict__ ip4, int32_t* __restrict__ ip6, uint32_t* __restrict__ pf,
+                         int64_t* __restrict__ ts) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t j = perm[i];
+  id[i] = in.id[j];
+  pid[i] = in.pid[j];
+  lsvc[i] = in.lsvc[j];
+  rsvc[i] = in.rsvc[j];
+  ip4[i] = in.ip4[j];
+  ip6[i] = in.ip6[j];
+  pf[i] = in.pf[j];
+  if (ts) ts[i] = in.ts[j];
+}
+
 // The mapped pinned buffer of ordered link output (S*S <= COMPACT_WG * 8).
 static hipError_t ensure_map(zdl_ctx* c) {
   if (c->h_map) return hipSuccess;
@@ -723,7 +754,7 @@ static hipError_t ensure_map(zdl_ctx* c) {
 // windows it queued, takes the traces it listed as longer than WSMALL and (small tables)
 // compacts the table into the mapped buffer zdl_link reads.
 static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans, const uint64_t* off,
-                          uint64_t n_traces) {
+                          uint64_t n_traces, const uint64_t* n_traces_dev = nullptr) {
   const size_t SS = (size_t)c->S * c->S;
   const int dense = SS <= (size_t)WDENSE_MAX;
   const int grid = c->grid, lgrid = c->cus * lk::wgs_per_cu;  // k_link: two 16-wave workgroups per CU
@@ -733,7 +764,8 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   A.c = Cols{col->id, col->parent_id, col->local_svc, col->remote_svc, col->local_ip4, col->local_ip6,
              col->port_flags, col->timestamp};
   A.off = off;
-  A.n_traces = n_traces;
+  A.n_traces = n_traces;  // with n_traces_dev: an upper bound (sizes the queues)
+  A.n_traces_dev = n_traces_dev;
   A.n_spans = n_spans;
   A.R = Ranks{c->nrank[0] ? c->rank[0].p : nullptr, c->nrank[1] ? c->rank[1].p : nullptr,
               c->nrank[2] ? c->rank[2].p : nullptr, c->nrank[0], c->nrank[1], c->nrank[2]};
@@ -798,16 +830,49 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   return ZDL_OK;
 }
 
+// Ungrouped device columns: group by trace_lo (zdl_group.hip), gather the columns into
+// grouped order, link with the device-side trace count.
+static int put_spans_ungrouped(zdl_ctx* c, const zdl_span_cols* col, uint64_t n) {
+  if (!col->trace_lo) return fail(c, ZDL_EINVAL, "ungrouped input needs the trace_lo column");
+  if (n >= (1ull << 32)) return fail(c, ZDL_EINVAL, "ungrouped input too large (n_spans >= 2^32)");
+  HIP_TRY(c, group_spans(c->grp, col->trace_lo, col->ord, n, c->stream));
+  HIP_TRY(c, c->g_id.ensure(n));
+  HIP_TRY(c, c->g_pid.ensure(n));
+  HIP_TRY(c, c->g_lsvc.ensure(n));
+  HIP_TRY(c, c->g_rsvc.ensure(n));
+  HIP_TRY(c, c->g_ip4.ensure(n));
+  HIP_TRY(c, c->g_ip6.ensure(n));
+  HIP_TRY(c, c->g_pf.ensure(n));
+  if (c->window) HIP_TRY(c, c->g_ts.ensure(n));
+  const Cols in{col->id, col->parent_id, col->local_svc, col->remote_svc, col->local_ip4, col->local_ip6,
+                col->port_flags, c->window ? col->timestamp : nullptr};
+  hipLaunchKernelGGL(k_gather, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, in, c->grp.perm, n,
+                     c->g_id.p, c->g_pid.p, c->g_lsvc.p, c->g_rsvc.p, c->g_ip4.p, c->g_ip6.p, c->g_pf.p,
+                     c->window ? c->g_ts.p : nullptr);
+  HIP_TRY(c, hipGetLastError());
+  zdl_span_cols g{};
+  g.id = c->g_id.p;
+  g.parent_id = c->g_pid.p;
+  g.local_svc = c->g_lsvc.p;
+  g.remote_svc = c->g_rsvc.p;
+  g.local_ip4 = c->g_ip4.p;
+  g.local_ip6 = c->g_ip6.p;
+  g.port_flags = c->g_pf.p;
+  g.timestamp = c->window ? c->g_ts.p : nullptr;
+  return put_spans_link(c, &g, n, c->grp.off, n, c->grp.count);
+}
+
 int zdl_put_spans_device(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans, const uint64_t* off,
                          uint64_t n_traces) {
   if (!c || !col) return fail(c, ZDL_EINVAL, "null argument");
-  if (n_traces == 0 || n_spans == 0) return ZDL_OK;
+  if (n_spans == 0 || (off && n_traces == 0)) return ZDL_OK;
   if (!col->id || !col->parent_id || !col->local_svc || !col->remote_svc || !col->local_ip4 ||
-      !col->local_ip6 || !col->port_flags || !off)
+      !col->local_ip6 || !col->port_flags)
     return fail(c, ZDL_EINVAL, "missing column");
   if (c->window && !col->timestamp) return fail(c, ZDL_EINVAL, "window set but no timestamp column");
   if (n_traces >= 0xffffffffull || n_spans >= (1ull << 40)) return fail(c, ZDL_EINVAL, "input too large");
   HIP_TRY(c, enter(c));
+  if (!off) return put_spans_ungrouped(c, col, n_spans);
   return put_spans_link(c, col, n_spans, off, n_traces);
 }
 
@@ -823,11 +888,15 @@ int zdl_sync(zdl_ctx* c) {
 
 int zdl_put_spans(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans, const uint64_t* off,
                   uint64_t n_traces) {
-  if (!c || !col || (!off && n_traces)) return fail(c, ZDL_EINVAL, "null argument");
-  if (n_traces == 0) return ZDL_OK;
-  if (off[0] != 0 || off[n_traces] != n_spans) return fail(c, ZDL_EINVAL, "trace offsets must span [0, n_spans]");
-  for (uint64_t t = 0; t < n_traces; ++t)
-    if (off[t + 1] < off[t]) return fail(c, ZDL_EINVAL, "trace offsets are not non-decreasing");
+  if (!c || !col) return fail(c, ZDL_EINVAL, "null argument");
+  if (off) {
+    if (n_traces == 0) return ZDL_OK;
+    if (off[0] != 0 || off[n_traces] != n_spans) return fail(c, ZDL_EINVAL, "trace offsets must span [0, n_spans]");
+    for (uint64_t t = 0; t < n_traces; ++t)
+      if (off[t + 1] < off[t]) return fail(c, ZDL_EINVAL, "trace offsets are not non-decreasing");
+  } else if (!col->trace_lo) {
+    return fail(c, ZDL_EINVAL, "ungrouped input needs the trace_lo column");
+  }
   if (n_spans == 0) return ZDL_OK;
   HIP_TRY(c, enter(c));
   HIP_TRY(c, c->h_id.ensure(n_spans));
@@ -837,7 +906,7 @@ int zdl_put_spans(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans, const 
   HIP_TRY(c, c->h_ip4.ensure(n_spans));
   HIP_TRY(c, c->h_ip6.ensure(n_spans));
   HIP_TRY(c, c->h_pf.ensure(n_spans));
-  HIP_TRY(c, c->h_off.ensure(n_traces + 1));
+  if (off) HIP_TRY(c, c->h_off.ensure(n_traces + 1));
   hipStream_t s = c->stream;
   HIP_TRY(c, hipMemcpyAsync(c->h_id.p, col->id, n_spans * 8, hipMemcpyHostToDevice, s));
   HIP_TRY(c, hipMemcpyAsync(c->h_pid.p, col->parent_id, n_spans * 8, hipMemcpyHostToDevice, s));
@@ -846,9 +915,19 @@ int zdl_put_spans(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans, const 
   HIP_TRY(c, hipMemcpyAsync(c->h_ip4.p, col->local_ip4, n_spans * 4, hipMemcpyHostToDevice, s));
   HIP_TRY(c, hipMemcpyAsync(c->h_ip6.p, col->local_ip6, n_spans * 4, hipMemcpyHostToDevice, s));
   HIP_TRY(c, hipMemcpyAsync(c->h_pf.p, col->port_flags, n_spans * 4, hipMemcpyHostToDevice, s));
-  HIP_TRY(c, hipMemcpyAsync(c->h_off.p, off, (n_traces + 1) * 8, hipMemcpyHostToDevice, s));
   zdl_span_cols d{};
-  d.trace_lo = nullptr;
+  if (off) {
+    HIP_TRY(c, hipMemcpyAsync(c->h_off.p, off, (n_traces + 1) * 8, hipMemcpyHostToDevice, s));
+  } else {  // grouped on the device
+    HIP_TRY(c, c->h_lo.ensure(n_spans));
+    HIP_TRY(c, hipMemcpyAsync(c->h_lo.p, col->trace_lo, n_spans * 8, hipMemcpyHostToDevice, s));
+    d.trace_lo = c->h_lo.p;
+    if (col->ord) {
+      HIP_TRY(c, c->h_ord.ensure(n_spans));
+      HIP_TRY(c, hipMemcpyAsync(c->h_ord.p, col->ord, n_spans * 4, hipMemcpyHostToDevice, s));
+      d.ord = c->h_ord.p;
+    }
+  }
   d.id = c->h_id.p;
   d.parent_id = c->h_pid.p;
   d.local_svc = c->h_lsvc.p;
@@ -862,7 +941,7 @@ int zdl_put_spans(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans, const 
     HIP_TRY(c, hipMemcpyAsync(c->h_ts.p, col->timestamp, n_spans * 8, hipMemcpyHostToDevice, s));
     d.timestamp = c->h_ts.p;
   }
-  int rc = zdl_put_spans_device(c, &d, n_spans, c->h_off.p, n_traces);
+  int rc = zdl_put_spans_device(c, &d, n_spans, off ? c->h_off.p : nullptr, n_traces);
   if (rc != ZDL_OK) return rc;
   return zdl_sync(c);
 }

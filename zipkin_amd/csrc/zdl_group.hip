@@ -1,0 +1,116 @@
+// zdl_group.hip — on-device grouping of ungrouped spans by low trace id (zdl_group.h).
+#include "zdl_group.h"
+
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+
+namespace zdl {
+namespace {
+
+__global__ void k_iota(uint32_t* __restrict__ idx, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) idx[i] = (uint32_t)i;
+}
+
+__global__ void k_take_keys(const uint64_t* __restrict__ trace_lo, const uint32_t* __restrict__ idx,
+                            uint64_t* __restrict__ keys, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) keys[i] = trace_lo[idx[i]];
+}
+
+// flag[i] = 1 where a new trace starts in the sorted keys
+__global__ void k_heads(const uint64_t* __restrict__ keys, uint64_t n, uint8_t* __restrict__ flag) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) flag[i] = i == 0 || keys[i] != keys[i - 1];
+}
+
+__global__ void k_close(uint64_t* __restrict__ off, const uint64_t* __restrict__ count, uint64_t n) {
+  if (threadIdx.x == 0) off[*count] = n;
+}
+
+template <class T>
+hipError_t grow(T*& p, size_t n) {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  return hipMalloc((void**)&p, std::max<size_t>(n, 1) * sizeof(T));
+}
+
+inline dim3 blocks(uint64_t n) { return dim3((unsigned)((n + 255) / 256)); }
+
+}  // namespace
+
+void GroupWork::release() {
+  for (auto*& p : keys) { if (p) (void)hipFree(p); p = nullptr; }
+  for (auto*& p : idx) { if (p) (void)hipFree(p); p = nullptr; }
+  for (auto*& p : ord_keys) { if (p) (void)hipFree(p); p = nullptr; }
+  if (off) (void)hipFree(off);
+  if (count) (void)hipFree(count);
+  if (tmp) (void)hipFree(tmp);
+  off = nullptr;
+  count = nullptr;
+  tmp = nullptr;
+  tmp_bytes = 0;
+  perm = nullptr;
+  cap = 0;
+}
+
+#define GTRY(expr)                          \
+  do {                                      \
+    hipError_t _e = (expr);                 \
+    if (_e != hipSuccess) return _e;        \
+  } while (0)
+
+hipError_t group_spans(GroupWork& g, const uint64_t* trace_lo, const uint32_t* ord, uint64_t n,
+                       hipStream_t s) {
+  if (n == 0 || n >= (1ull << 32)) return hipErrorInvalidValue;
+  if (n > g.cap) {
+    for (int b = 0; b < 2; ++b) {
+      GTRY(grow(g.keys[b], n));
+      GTRY(grow(g.idx[b], n));
+      GTRY(grow(g.ord_keys[b], n));
+    }
+    GTRY(grow(g.off, n + 1));
+    if (!g.count) GTRY(hipMalloc((void**)&g.count, sizeof(uint64_t)));
+    // scratch: the larger of the two sorts and the run-head selection (flags live in ord_keys[1])
+    size_t a = 0, b = 0, c = 0;
+    GTRY(hipcub::DeviceRadixSort::SortPairs(nullptr, a, g.keys[0], g.keys[1], g.idx[0], g.idx[1], (int)n, 0, 64, s));
+    GTRY(hipcub::DeviceRadixSort::SortPairs(nullptr, b, g.ord_keys[0], g.ord_keys[1], g.idx[0], g.idx[1], (int)n, 0,
+                                            32, s));
+    GTRY(hipcub::DeviceSelect::Flagged(nullptr, c, hipcub::CountingInputIterator<uint64_t>(0),
+                                       reinterpret_cast<uint8_t*>(g.ord_keys[1]), g.off, g.count, (int)n, s));
+    const size_t need = std::max(a, std::max(b, c));
+    if (need > g.tmp_bytes) {
+      if (g.tmp) (void)hipFree(g.tmp);
+      g.tmp = nullptr;
+      g.tmp_bytes = 0;
+      GTRY(hipMalloc(&g.tmp, need));
+      g.tmp_bytes = need;
+    }
+    g.cap = n;
+  }
+  hipLaunchKernelGGL(k_iota, blocks(n), dim3(256), 0, s, g.idx[0], n);
+  GTRY(hipGetLastError());
+  size_t bytes = g.tmp_bytes;
+  const uint32_t* idx_in = g.idx[0];
+  if (ord) {  // storage order first (stable), then the trace key (stable) keeps it
+    GTRY(hipcub::DeviceRadixSort::SortPairs(g.tmp, bytes, ord, g.ord_keys[0], g.idx[0], g.idx[1], (int)n, 0, 32, s));
+    idx_in = g.idx[1];
+  }
+  hipLaunchKernelGGL(k_take_keys, blocks(n), dim3(256), 0, s, trace_lo, idx_in, g.keys[0], n);
+  GTRY(hipGetLastError());
+  uint32_t* idx_out = ord ? g.idx[0] : g.idx[1];
+  bytes = g.tmp_bytes;
+  GTRY(hipcub::DeviceRadixSort::SortPairs(g.tmp, bytes, g.keys[0], g.keys[1], idx_in, idx_out, (int)n, 0, 64, s));
+  g.perm = idx_out;
+  uint8_t* flag = reinterpret_cast<uint8_t*>(g.ord_keys[1]);
+  hipLaunchKernelGGL(k_heads, blocks(n), dim3(256), 0, s, g.keys[1], n, flag);
+  GTRY(hipGetLastError());
+  bytes = g.tmp_bytes;
+  GTRY(hipcub::DeviceSelect::Flagged(g.tmp, bytes, hipcub::CountingInputIterator<uint64_t>(0), flag, g.off, g.count,
+                                     (int)n, s));
+  hipLaunchKernelGGL(k_close, dim3(1), dim3(64), 0, s, g.off, g.count, n);
+  return hipGetLastError();
+}
+
+}  // namespace zdl
