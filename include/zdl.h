@@ -68,11 +68,19 @@ extern "C" {
 /* ---- output order for zdl_link ---- */
 #define ZDL_ORDER_SORTED      0  /* by (rank[parent], rank[child]) */
 #define ZDL_ORDER_FIRST_SEEN  1  /* only for zdl_merge_links output: DependencyLinker.merge order */
+#define ZDL_ORDER_INSERTION   2  /* DependencyLinker.link() order: the LinkedHashMap insertion order of
+                                    addLink (DependencyLinker.java:166-186) over the puts' traces in
+                                    order, each tree breadth-first (SpanNode.java:64-89). Needs a
+                                    context created with ZDL_FLAG_INSERTION_ORDER. */
 
 /* ---- context flags ---- */
 #define ZDL_FLAG_TIMING  1u      /* HIP events around k_link only: zdl_kernel_times.tiles_ms = mean of the
                                     puts since the previous zdl_get_kernel_times (last <= 64) */
 #define ZDL_FLAG_TIMING_ALL 2u   /* record HIP events around every kernel (all zdl_kernel_times fields) */
+#define ZDL_FLAG_INSERTION_ORDER 4u  /* keep, per (parent, child), the rank of its first addLink so that
+                                        zdl_link can return ZDL_ORDER_INSERTION; puts take the exact
+                                        per-trace path (slower than the default streaming path); traces
+                                        are limited to 2^21 spans */
 
 /*
  * Span columns, structure of arrays, n_spans entries each. A local endpoint is
@@ -157,7 +165,8 @@ int zdl_put_spans_device(zdl_ctx* ctx, const zdl_span_cols* dev_cols, uint64_t n
 int zdl_sync(zdl_ctx* ctx);
 
 /* DependencyLinker.link(): materialise the accumulated counts. The context keeps
- * them (link() may be called again, like the reference). order: ZDL_ORDER_SORTED. */
+ * them (link() may be called again, like the reference). order: ZDL_ORDER_SORTED, or
+ * ZDL_ORDER_INSERTION on a ZDL_FLAG_INSERTION_ORDER context (the reference's list order). */
 int zdl_link(zdl_ctx* ctx, int order, zdl_links* out);
 
 /* DependencyLinker.merge(links): sums call/error counts per (parent, child) of the n
@@ -170,7 +179,8 @@ int zdl_merge_links(zdl_ctx* ctx, const int32_t* parent, const int32_t* child,
 /* Adds n pre-aggregated links to the context's accumulated counts (what
  * DependencyLinker.merge does for stores that keep daily links, e.g.
  * cassandra SelectDependencies.java:75-91); used when a context is re-created with a
- * larger service dictionary. Synchronous. */
+ * larger service dictionary. On a ZDL_FLAG_INSERTION_ORDER context the n links count as
+ * first seen in their input order, before anything put afterwards. Synchronous. */
 int zdl_add_links(zdl_ctx* ctx, const int32_t* parent, const int32_t* child,
                   const int64_t* call_count, const int64_t* error_count, uint64_t n);
 
@@ -178,7 +188,8 @@ int zdl_add_links(zdl_ctx* ctx, const int32_t* parent, const int32_t* child,
 int zdl_reset(zdl_ctx* ctx);
 
 /* Multi-GPU combine support: copy the S x S int64 call and error tables to/from device
- * buffers of the same device (e.g. for an RCCL all-reduce), ordered on the ctx stream. */
+ * buffers of the same device (e.g. for an RCCL all-reduce), ordered on the ctx stream.
+ * zdl_table_import is refused on a ZDL_FLAG_INSERTION_ORDER context (no first-seen ranks). */
 int zdl_table_export(zdl_ctx* ctx, void* dev_call, void* dev_err);
 int zdl_table_import(zdl_ctx* ctx, const void* dev_call, const void* dev_err);
 

@@ -13,9 +13,10 @@ LIB_PATH = os.path.join(HERE, "libzdl.so")
 
 ZDL_OK, ZDL_EINVAL, ZDL_ENOMEM, ZDL_EDEVICE, ZDL_EREF_NPE, ZDL_EREF_IAE = 0, -1, -2, -3, -4, -5
 ZDL_DICT_SERVICE, ZDL_DICT_IPV4, ZDL_DICT_IPV6 = 0, 1, 2
-ZDL_ORDER_SORTED, ZDL_ORDER_FIRST_SEEN = 0, 1
+ZDL_ORDER_SORTED, ZDL_ORDER_FIRST_SEEN, ZDL_ORDER_INSERTION = 0, 1, 2
 ZDL_FLAG_TIMING = 1
 ZDL_FLAG_TIMING_ALL = 2
+ZDL_FLAG_INSERTION_ORDER = 4
 
 PF_KIND_SHIFT = 16
 PF_SHARED_SHIFT = 19
@@ -117,15 +118,17 @@ class Context:
     """One zdl_ctx: a device-resident link-count table for S services."""
 
     def __init__(self, n_services: int, device: int = 0, timing: bool = False, timing_all: bool = False,
-                 timing_stride: int = 1):
+                 timing_stride: int = 1, insertion_order: bool = False):
         L = lib()
         flags = (ZDL_FLAG_TIMING if timing else 0) | (ZDL_FLAG_TIMING_ALL if timing_all else 0)
+        flags |= ZDL_FLAG_INSERTION_ORDER if insertion_order else 0
         cfg = Config(device, int(n_services), flags, int(timing_stride))
         h = L.zdl_create(C.byref(cfg))
         if not h:
             raise ZdlError(ZDL_EDEVICE, L.zdl_create_error().decode())
         self.h = C.c_void_p(h)
         self.n_services = int(n_services)
+        self.insertion_order = bool(insertion_order)
         self._L = L
 
     def close(self):
@@ -190,9 +193,11 @@ class Context:
                 np.ctypeslib.as_array(out.call_count, (n,)).copy(),
                 np.ctypeslib.as_array(out.error_count, (n,)).copy())
 
-    def link(self):
+    def link(self, order: int = ZDL_ORDER_SORTED):
+        """(parent, child, call, err) arrays; order ZDL_ORDER_SORTED or, on an
+        insertion_order context, ZDL_ORDER_INSERTION (DependencyLinker.link()'s order)."""
         out = Links()
-        self.check(self._L.zdl_link(self.h, ZDL_ORDER_SORTED, C.byref(out)))
+        self.check(self._L.zdl_link(self.h, int(order), C.byref(out)))
         return self._links_to_numpy(out)
 
     def merge_links(self, parent, child, call, err):

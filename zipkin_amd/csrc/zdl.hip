@@ -88,6 +88,14 @@ struct Args {
   int32_t* b_parent;
   uint8_t* b_live;
   uint8_t* b_haschild;
+  // insertion order (ZDL_FLAG_INSERTION_ORDER): first-addLink ranks per cell (ord_min),
+  // the put-global position of this put's span 0, and big-trace breadth-first scratch
+  unsigned long long* first;
+  uint64_t span_base;
+  unsigned long long* o_key;
+  uint32_t* o_fa;
+  uint32_t* o_fb;
+  uint32_t* o_bfs;
 };
 
 #include "zdl_full.inc"  // the full per-window emulation (k_tail's first part)
@@ -99,6 +107,130 @@ struct Args {
 // ranks.
 __device__ __forceinline__ void big_sync() { __syncthreads(); }
 
+// Exclusive scan of one value per thread over the workgroup (BIG_WG threads); *total gets
+// the sum. Every thread must call.
+__device__ __forceinline__ uint32_t big_scan(uint32_t x, uint32_t* total) {
+  __shared__ uint32_t ws[BIG_WG / 64 + 1];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t incl = x;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += y;
+  }
+  if (lane == 63) ws[w] = incl;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+    for (int i = 0; i < BIG_WG / 64; ++i) {
+      const uint32_t t = ws[i];
+      ws[i] = acc;
+      acc += t;
+    }
+    ws[BIG_WG / 64] = acc;
+  }
+  __syncthreads();
+  const uint32_t r = ws[w] + incl - x;
+  *total = ws[BIG_WG / 64];
+  __syncthreads();
+  return r;
+}
+
+// First position >= `from` whose sorted key is >= k (keys ascending over [0, n)).
+__device__ __forceinline__ uint32_t big_lower(const unsigned long long* key, uint32_t n, unsigned long long k) {
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (key[mid] < k) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+// Insertion order for one big trace: the breadth-first index of every node reachable
+// from the root (SpanNode.traverse, SpanNode.java:64-89) into bfs[]. Children lists are the
+// nodes sorted by (parent, spanToParent entry position) - see wave_bfs for the entry
+// rule; the synthetic root is position n. Then level by level: a frontier in
+// breadth-first order, each node's children appended at a scanned offset.
+__device__ __forceinline__ void big_bfs(const View& v, int n, int rp, unsigned long long* key, uint32_t* fa,
+                                        uint32_t* fb, uint32_t* bfs) {
+  constexpr unsigned long long M21 = (1ull << 21) - 1;
+  for (int p = threadIdx.x; p < n; p += BIG_WG) {
+    unsigned long long k = ~0ull;
+    const int par = v.parent[p];
+    if (v.live[p] && par != PAR_NONMEMBER) {
+      const uint32_t s = v.perm[p];
+      const uint64_t my = v.id[s];
+      int gb = p;
+      while (gb > 0 && v.id[v.perm[gb - 1]] == my) --gb;
+      int ge = p + 1;
+      while (ge < n && v.id[v.perm[ge]] == my) ++ge;
+      int ek = p;
+      if (is_shared(v.pf[s])) {
+        for (int q = gb; q < p; ++q)
+          if (v.live[q] && is_shared(v.pf[v.perm[q]]) && local_eq(v, v.perm[q], s)) { ek = q; break; }
+      } else if (rp >= gb && rp < ge) {
+        ek = n;
+      } else {
+        for (int q = gb; q < p; ++q)
+          if (v.live[q] && !is_shared(v.pf[v.perm[q]])) { ek = q; break; }
+      }
+      const unsigned long long pp = par >= 0 ? (unsigned long long)par : (unsigned long long)n;
+      k = (pp << 42) | ((unsigned long long)ek << 21) | (unsigned long long)p;
+    }
+    key[p] = k;
+  }
+  big_sync();
+  int npad = 1;
+  while (npad < n) npad <<= 1;
+  for (int kk = 2; kk <= npad; kk <<= 1) {  // ascending bitonic (any n: absent partners are +inf)
+    for (int jj = kk - 1; jj > 0; jj = (jj == kk - 1 ? kk >> 2 : jj >> 1)) {
+      for (int i = threadIdx.x; i < n; i += BIG_WG) {
+        const int l = i ^ jj;
+        if (l > i && l < n) {
+          const unsigned long long a = key[i], b = key[l];
+          if (b < a) { key[i] = b; key[l] = a; }
+        }
+      }
+      big_sync();
+    }
+  }
+  __shared__ uint32_t sh_f;
+  if (threadIdx.x == 0) {
+    fa[0] = rp >= 0 ? (uint32_t)rp : (uint32_t)n;
+    if (rp >= 0) bfs[rp] = 0;
+    sh_f = 1;
+  }
+  big_sync();
+  uint32_t fsz = sh_f, next = rp >= 0 ? 1u : 0u;
+  while (fsz != 0) {
+    uint32_t gsz = 0;
+    for (uint32_t i0 = 0; i0 < fsz; i0 += BIG_WG) {
+      const uint32_t i = i0 + threadIdx.x;
+      uint32_t lo = 0, cnt = 0;
+      if (i < fsz) {
+        const unsigned long long u = fa[i];
+        lo = big_lower(key, (uint32_t)n, u << 42);
+        cnt = big_lower(key, (uint32_t)n, (u + 1) << 42) - lo;
+      }
+      uint32_t tot;
+      const uint32_t o = gsz + big_scan(cnt, &tot);
+      for (uint32_t j = 0; j < cnt; ++j) {
+        const uint32_t node = (uint32_t)(key[lo + j] & M21);
+        fb[o + j] = node;
+        bfs[node] = next + o + j;
+      }
+      gsz += tot;
+    }
+    big_sync();
+    next += gsz;
+    fsz = gsz;
+    uint32_t* t = fa;
+    fa = fb;
+    fb = t;
+  }
+}
+
+template <int ORD>
 __device__ __forceinline__ void big_traces(const Args& A) {
   __shared__ int32_t sh_root;
   __shared__ int sh_act;
@@ -227,13 +359,25 @@ __device__ __forceinline__ void big_traces(const Args& A) {
       if (q >= 0) v.haschild[q] = 1;
     }
     big_sync();
+    uint32_t* bfs = nullptr;
+    if (ORD) {
+      if (n >= (1 << 21) - 1) {  // ranks pack positions in 21 bits
+        if (threadIdx.x == 0) atomicOr(A.status, ST_ORDLIM);
+        big_sync();
+        continue;
+      }
+      bfs = A.o_bfs + b;
+      big_bfs(v, n, rp, A.o_key + b, A.o_fa + b, A.o_fb + b, bfs);
+      big_sync();
+    }
     for (int p = threadIdx.x; p < n; p += BIG_WG) {
       if (v.parent[p] == PAR_NONMEMBER) continue;
-      link_node(v, p, rp, n, [&](int32_t a, int32_t c, bool e) {
+      link_node(v, p, rp, n, [&](int32_t a, int32_t c, bool e, int k) {
         if ((uint32_t)a >= A.S || (uint32_t)c >= A.S) { atomicOr(A.status, ST_BADSVC); return; }
         const size_t idx = (size_t)a * A.S + c;
         atomicAdd(&A.call[idx], 1ull);
         if (e) atomicAdd(&A.err[idx], 1ull);
+        if (ORD) ord_min(A.first, A.S, a, c, ord_rank(A.span_base + b, bfs[p], k));
       });
     }
     big_sync();
@@ -339,7 +483,7 @@ __global__ void __launch_bounds__(COMPACT_WG) k_compact_ordered(const unsigned l
 static_assert(TAIL_WG == BIG_WG && TAIL_WG == COMPACT_WG, "k_tail runs all three parts");
 inline size_t tail_block_bytes(int window) { return WTABLE_BYTES + (TAIL_WG / 64) * wl::bytes(window); }
 
-template <int DENSE, int WINDOW>
+template <int DENSE, int WINDOW, int ORD>
 __global__ void __launch_bounds__(TAIL_WG, 1) k_tail(Args A) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   __shared__ bool last;
@@ -347,9 +491,9 @@ __global__ void __launch_bounds__(TAIL_WG, 1) k_tail(Args A) {
     *A.cx_count_next = 0;
     *A.big_count_next = 0;
   }
-  full_windows<DENSE, WINDOW, TAIL_WG / 64>(A, lds);
+  full_windows<DENSE, WINDOW, TAIL_WG / 64, ORD>(A, lds);
   __syncthreads();
-  big_traces(A);
+  big_traces<ORD>(A);
   if (!A.map) return;
   // The table and status atomics are performed at the device-coherent level; waiting for
   // this workgroup's to complete (vmcnt) before counting it done is enough, and the last
@@ -364,9 +508,13 @@ __global__ void __launch_bounds__(TAIL_WG, 1) k_tail(Args A) {
   if (threadIdx.x == 0) *A.done = 0;
 }
 
-inline const void* k_tail_fn(int dense, int window) {
-  if (dense) return window ? (const void*)k_tail<1, 1> : (const void*)k_tail<1, 0>;
-  return window ? (const void*)k_tail<0, 1> : (const void*)k_tail<0, 0>;
+inline const void* k_tail_fn(int dense, int window, int ord = 0) {
+  if (ord) {
+    if (dense) return window ? (const void*)k_tail<1, 1, 1> : (const void*)k_tail<1, 0, 1>;
+    return window ? (const void*)k_tail<0, 1, 1> : (const void*)k_tail<0, 0, 1>;
+  }
+  if (dense) return window ? (const void*)k_tail<1, 1, 0> : (const void*)k_tail<1, 0, 0>;
+  return window ? (const void*)k_tail<0, 1, 0> : (const void*)k_tail<0, 0, 0>;
 }
 
 // Any S: non-zero cells -> records in arbitrary order (the host sorts them).
@@ -387,14 +535,14 @@ __global__ void k_merge_accum(const int32_t* __restrict__ p, const int32_t* __re
                               const int64_t* __restrict__ call, const int64_t* __restrict__ err, uint64_t n,
                               uint32_t S, unsigned long long* __restrict__ tcall,
                               unsigned long long* __restrict__ terr, unsigned long long* __restrict__ tfirst,
-                              uint32_t* __restrict__ status) {
+                              uint32_t* __restrict__ status, uint64_t first_base, int first_shift) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   if ((uint32_t)p[i] >= S || (uint32_t)c[i] >= S) { atomicOr(status, ST_BADSVC); return; }
   const size_t idx = (size_t)p[i] * S + c[i];
   atomicAdd(&tcall[idx], (unsigned long long)call[i]);
   atomicAdd(&terr[idx], (unsigned long long)err[i]);
-  atomicMin(&tfirst[idx], (unsigned long long)i);
+  atomicMin(&tfirst[idx], (unsigned long long)(first_base + i) << first_shift);
 }
 
 __global__ void k_merge_compact(const unsigned long long* __restrict__ tcall, const unsigned long long* __restrict__ terr,
@@ -460,6 +608,12 @@ struct zdl_ctx {
   // S x S counters
   DevBuf<unsigned long long> call, errc;
   DevBuf<uint32_t> status;
+  // insertion order (ZDL_FLAG_INSERTION_ORDER): first-addLink rank per cell, the put-global
+  // position of the next put's span 0, big-trace breadth-first scratch
+  bool ord = false;
+  DevBuf<unsigned long long> first, o_key;
+  uint64_t span_base = 0;
+  DevBuf<uint32_t> o_fa, o_fb, o_bfs;
   // per-put scratch
   DevBuf<uint32_t> big_list, counters;  // counters: big[2], cx[2], alternating by put
   uint32_t epoch = 0;
@@ -544,6 +698,7 @@ int status_code(zdl_ctx* c, uint32_t st) {
   if (st & ST_BADSVC) return fail(c, ZDL_EINVAL, "service id >= n_services");
   if (st & ST_BADOFF) return fail(c, ZDL_EINVAL, "trace offsets are not non-decreasing");
   if (st & ST_INTERNAL) return fail(c, ZDL_EDEVICE, "internal consistency check failed on the device");
+  if (st & ST_ORDLIM) return fail(c, ZDL_EINVAL, "insertion order: a trace has more than 2^21 - 2 spans");
   return ZDL_OK;
 }
 
@@ -597,6 +752,7 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
   c->device = cfg->device;
   c->S = cfg->n_services;
   c->flags = cfg->flags;
+  c->ord = (cfg->flags & ZDL_FLAG_INSERTION_ORDER) != 0;
   c->lk_stride = std::max<uint32_t>(1u, cfg->timing_stride);
   hipError_t e = hipSetDevice(c->device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
@@ -608,6 +764,8 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
   if (e == hipSuccess) e = hipMemset(c->call.p, 0, SS * 8);
   if (e == hipSuccess) e = hipMemset(c->errc.p, 0, SS * 8);
   if (e == hipSuccess) e = hipMemset(c->status.p, 0, 16);
+  if (e == hipSuccess && c->ord) e = c->first.ensure(SS);
+  if (e == hipSuccess && c->ord) e = hipMemset(c->first.p, 0xff, SS * 8);
   if (e == hipSuccess) e = c->counters.ensure(5);  // + k_tail's finished-workgroup count
   if (e == hipSuccess) e = hipMemset(c->counters.p, 0, 20);
   if (e == hipSuccess) e = hipHostMalloc((void**)&c->h_meta, 16, hipHostMallocDefault);
@@ -629,7 +787,10 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
         e = hipFuncSetAttribute(k_link_fn(1, 0, m), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)link_block_bytes(0));
       if (e == hipSuccess)
-        e = hipFuncSetAttribute(k_tail_fn(d, w), hipFuncAttributeMaxDynamicSharedMemorySize,
+        e = hipFuncSetAttribute(k_link_fn(d, w, 3), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)link_block_bytes(w));
+      for (int o = 0; o < 2 && e == hipSuccess; ++o)
+        e = hipFuncSetAttribute(k_tail_fn(d, w, o), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)tail_block_bytes(w));
     }
   if (e == hipSuccess) {
@@ -656,6 +817,7 @@ void zdl_destroy(zdl_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (auto& r : c->rank) r.release();
   c->call.release(); c->errc.release(); c->status.release();
+  c->first.release(); c->o_key.release(); c->o_fa.release(); c->o_fb.release(); c->o_bfs.release();
   c->big_list.release(); c->counters.release();
   c->cx_win.release();
   if (c->prof_on && c->prof.p) {
@@ -790,7 +952,8 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   void* kargs[] = {&A};
   ev_record(c, 0);
   ev_record(c, 1);
-  HIP_TRY(c, hipLaunchKernel(k_link_fn(dense, c->window, c->prof_on ? 1 : (c->skip ? 2 : 0)), dim3(lgrid),
+  const int lmode = c->ord ? 3 : (c->prof_on ? 1 : (c->skip ? 2 : 0));
+  HIP_TRY(c, hipLaunchKernel(k_link_fn(dense, c->window, lmode), dim3(lgrid),
                              dim3(lk::waves(c->window) * 64), kargs, link_block_bytes(c->window), c->stream));
   ev_record(c, 7);
   ev_record(c, 2);
@@ -817,12 +980,25 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   A.b_parent = c->b_parent.p;
   A.b_live = c->b_live.p;
   A.b_haschild = c->b_hasc.p;
-  const bool ordered = SS <= (size_t)COMPACT_WG * 8;
+  if (c->ord) {
+    HIP_TRY(c, c->o_key.ensure(n_spans));
+    HIP_TRY(c, c->o_fa.ensure(n_spans));
+    HIP_TRY(c, c->o_fb.ensure(n_spans));
+    HIP_TRY(c, c->o_bfs.ensure(n_spans));
+    A.first = c->first.p;
+    A.span_base = c->span_base;
+    A.o_key = c->o_key.p;
+    A.o_fa = c->o_fa.p;
+    A.o_fb = c->o_fb.p;
+    A.o_bfs = c->o_bfs.p;
+  }
+  const bool ordered = SS <= (size_t)COMPACT_WG * 8 && !c->ord;
   if (ordered) HIP_TRY(c, ensure_map(c));
   A.map = ordered && !getenv("ZDL_NOTAILMAP") ? c->d_map : nullptr;
   A.done = c->counters.p + 4;
-  HIP_TRY(c, hipLaunchKernel(k_tail_fn(dense, c->window), dim3(grid), dim3(TAIL_WG), kargs,
+  HIP_TRY(c, hipLaunchKernel(k_tail_fn(dense, c->window, c->ord ? 1 : 0), dim3(grid), dim3(TAIL_WG), kargs,
                              tail_block_bytes(c->window), c->stream));
+  c->span_base += n_spans;  // the next put's traces come after this one's
   ev_record(c, 4);
   ++c->epoch;  // k_tail zeroed the other counter slots
   c->map_fresh = A.map != nullptr;
@@ -951,7 +1127,8 @@ int zdl_reset(zdl_ctx* c) {
   HIP_TRY(c, enter(c));
   const size_t SS = (size_t)c->S * c->S;
   hipLaunchKernelGGL(k_zero_tables, dim3((unsigned)((SS + 255) / 256)), dim3(256), 0, c->stream, c->call.p,
-                     c->errc.p, (uint64_t)SS, c->status.p);
+                     c->errc.p, (uint64_t)SS, c->status.p, c->ord ? c->first.p : nullptr);
+  c->span_base = 0;
   HIP_TRY(c, hipGetLastError());
   c->map_fresh = false;
   return ZDL_OK;  // stream-ordered: no host wait
@@ -981,9 +1158,63 @@ static void sort_output(zdl_ctx* c, size_t n) {
   c->out_err.swap(er);
 }
 
+// zdl_link in ZDL_ORDER_INSERTION: the non-zero cells with their first-addLink ranks
+// (k_merge_compact over the context's tables), ordered by rank.
+static int link_insertion(zdl_ctx* c, zdl_links* out) {
+  const uint64_t SS = (uint64_t)c->S * c->S;
+  HIP_TRY(c, c->o_p.ensure(SS));
+  HIP_TRY(c, c->o_c.ensure(SS));
+  HIP_TRY(c, c->o_call.ensure(SS));
+  HIP_TRY(c, c->o_err.ensure(SS));
+  HIP_TRY(c, c->o_first.ensure(SS));
+  HIP_TRY(c, hipMemsetAsync(c->count.p, 0, 8, c->stream));
+  hipLaunchKernelGGL(k_merge_compact, dim3((unsigned)((SS + 255) / 256)), dim3(256), 0, c->stream, c->call.p,
+                     c->errc.p, c->first.p, SS, c->S, c->count.p, c->o_p.p, c->o_c.p, c->o_call.p, c->o_err.p,
+                     c->o_first.p);
+  HIP_TRY(c, hipGetLastError());
+  unsigned long long m = 0;
+  HIP_TRY(c, hipMemcpyAsync(&m, c->count.p, 8, hipMemcpyDeviceToHost, c->stream));
+  const int rc = zdl_sync(c);
+  if (rc != ZDL_OK) return rc;
+  std::vector<uint64_t> first(m);
+  std::vector<int32_t> p(m), ch(m);
+  std::vector<int64_t> ca(m), er(m);
+  if (m) {
+    HIP_TRY(c, hipMemcpy(p.data(), c->o_p.p, m * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(c, hipMemcpy(ch.data(), c->o_c.p, m * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(c, hipMemcpy(ca.data(), c->o_call.p, m * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(c, hipMemcpy(er.data(), c->o_err.p, m * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(c, hipMemcpy(first.data(), c->o_first.p, m * 8, hipMemcpyDeviceToHost));
+  }
+  std::vector<uint32_t> idx(m);
+  for (size_t i = 0; i < m; ++i) idx[i] = (uint32_t)i;
+  std::sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) { return first[a] < first[b]; });
+  c->out_p.resize(m);
+  c->out_c.resize(m);
+  c->out_call.resize(m);
+  c->out_err.resize(m);
+  for (size_t i = 0; i < m; ++i) {
+    c->out_p[i] = p[idx[i]];
+    c->out_c[i] = ch[idx[i]];
+    c->out_call[i] = ca[idx[i]];
+    c->out_err[i] = er[idx[i]];
+  }
+  out->n = m;
+  out->parent = c->out_p.data();
+  out->child = c->out_c.data();
+  out->call_count = c->out_call.data();
+  out->error_count = c->out_err.data();
+  return ZDL_OK;
+}
+
 int zdl_link(zdl_ctx* c, int order, zdl_links* out) {
   if (!c || !out) return ZDL_EINVAL;
-  if (order != ZDL_ORDER_SORTED) return fail(c, ZDL_EINVAL, "zdl_link supports ZDL_ORDER_SORTED");
+  if (order == ZDL_ORDER_INSERTION) {
+    if (!c->ord) return fail(c, ZDL_EINVAL, "ZDL_ORDER_INSERTION needs a ZDL_FLAG_INSERTION_ORDER context");
+    HIP_TRY(c, enter(c));
+    return link_insertion(c, out);
+  }
+  if (order != ZDL_ORDER_SORTED) return fail(c, ZDL_EINVAL, "zdl_link: order must be ZDL_ORDER_SORTED or ZDL_ORDER_INSERTION");
   HIP_TRY(c, enter(c));
   const uint64_t SS = (uint64_t)c->S * c->S;
   const bool ordered = SS <= (uint64_t)COMPACT_WG * 8;
@@ -1094,7 +1325,8 @@ int zdl_merge_links(zdl_ctx* c, const int32_t* parent, const int32_t* child, con
     HIP_TRY(c, hipMemcpyAsync(c->mi_call.p, call_count, n * 8, hipMemcpyHostToDevice, s));
     HIP_TRY(c, hipMemcpyAsync(c->mi_err.p, error_count, n * 8, hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(k_merge_accum, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, c->mi_p.p, c->mi_c.p,
-                       c->mi_call.p, c->mi_err.p, n, c->S, c->m_call.p, c->m_err.p, c->m_first.p, c->status.p);
+                       c->mi_call.p, c->mi_err.p, n, c->S, c->m_call.p, c->m_err.p, c->m_first.p, c->status.p,
+                       (uint64_t)0, 0);
     HIP_TRY(c, hipGetLastError());
   }
   hipLaunchKernelGGL(k_merge_compact, dim3((unsigned)((SS + 255) / 256)), dim3(256), 0, s, c->m_call.p, c->m_err.p,
@@ -1156,8 +1388,10 @@ int zdl_add_links(zdl_ctx* c, const int32_t* parent, const int32_t* child, const
   HIP_TRY(c, hipMemcpyAsync(c->mi_call.p, call_count, n * 8, hipMemcpyHostToDevice, s));
   HIP_TRY(c, hipMemcpyAsync(c->mi_err.p, error_count, n * 8, hipMemcpyHostToDevice, s));
   hipLaunchKernelGGL(k_merge_accum, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, c->mi_p.p, c->mi_c.p,
-                     c->mi_call.p, c->mi_err.p, n, c->S, c->call.p, c->errc.p, c->m_first.p, c->status.p);
+                     c->mi_call.p, c->mi_err.p, n, c->S, c->call.p, c->errc.p,
+                     c->ord ? c->first.p : c->m_first.p, c->status.p, c->ord ? c->span_base : 0, c->ord ? 24 : 0);
   HIP_TRY(c, hipGetLastError());
+  if (c->ord) c->span_base += n;  // the links rank before anything put afterwards
   c->map_fresh = false;
   return zdl_sync(c);
 }
@@ -1173,6 +1407,7 @@ int zdl_table_export(zdl_ctx* c, void* dev_call, void* dev_err) {
 
 int zdl_table_import(zdl_ctx* c, const void* dev_call, const void* dev_err) {
   if (!c || !dev_call || !dev_err) return ZDL_EINVAL;
+  if (c->ord) return fail(c, ZDL_EINVAL, "zdl_table_import: the table carries no insertion-order ranks");
   HIP_TRY(c, enter(c));
   const size_t bytes = (size_t)c->S * c->S * 8;
   HIP_TRY(c, hipMemcpyAsync(c->call.p, dev_call, bytes, hipMemcpyDeviceToDevice, c->stream));

@@ -21,7 +21,7 @@
 
 namespace zdl {
 
-enum : uint32_t { ST_NPE = 1u, ST_BADSVC = 2u, ST_BADOFF = 4u, ST_IAE = 8u, ST_INTERNAL = 16u };
+enum : uint32_t { ST_NPE = 1u, ST_BADSVC = 2u, ST_BADOFF = 4u, ST_IAE = 8u, ST_INTERNAL = 16u, ST_ORDLIM = 32u };
 enum : int32_t { PAR_TERMINAL = -1, PAR_NONMEMBER = -3 };
 
 template <class PermT, class ParT>
@@ -321,7 +321,8 @@ __device__ __forceinline__ void resolve_group(const V& v, int tb, int te, int gb
 }
 
 // DependencyLinker.putTrace's per-node rules (DependencyLinker.java:58-148) for the node
-// at position p; `emit(parent_svc, child_svc, is_error)` is addLink.
+// at position p; `emit(parent_svc, child_svc, is_error, k)` is addLink, k its order within
+// the node (0: the missing-link backfill, DependencyLinker.java:126-129; 1: the node's link).
 template <class V, class Emit>
 __device__ __forceinline__ void link_node(const V& v, int p, int rp, int n, Emit&& emit) {
   // reachability from the root and firstRemoteAncestor (DependencyLinker.java:153-164)
@@ -356,21 +357,35 @@ __device__ __forceinline__ void link_node(const V& v, int p, int rp, int n, Emit
   }
   bool is_error = err_of(pf);
   if (kind == ZDL_KIND_PRODUCER || kind == ZDL_KIND_CONSUMER) {
-    if (parent >= 0 && child >= 0) emit(parent, child, is_error);
+    if (parent >= 0 && child >= 0) emit(parent, child, is_error, 1);
     return;
   }
   if (ra >= 0) {
     const uint32_t as = v.perm[ra];
     const int32_t ran = v.lsvc[as];
     if (ran >= 0) {
-      if (kind == ZDL_KIND_CLIENT && svc >= 0 && ran != svc) emit(ran, svc, false);  // missing link
+      if (kind == ZDL_KIND_CLIENT && svc >= 0 && ran != svc) emit(ran, svc, false, 0);  // missing link
       if (kind == ZDL_KIND_SERVER || parent < 0) parent = ran;
       const uint64_t mypid = v.pid[s];
       if (!is_error && kind_of(v.pf[as]) == ZDL_KIND_CLIENT && mypid != 0 && mypid == v.id[as])
         is_error = err_of(v.pf[as]);
     }
   }
-  if (parent >= 0 && child >= 0) emit(parent, child, is_error);
+  if (parent >= 0 && child >= 0) emit(parent, child, is_error, 1);
+}
+
+// Insertion order (ZDL_FLAG_INSERTION_ORDER): first[cell] keeps the smallest rank of an
+// addLink of that (parent, child): (put-global position of the trace's first span) << 24
+// | (breadth-first index of the node << 1 | k). The plain load skips the atomic once a
+// smaller rank is in (ranks only decrease; a stale read only costs the atomic).
+__device__ __forceinline__ void ord_min(unsigned long long* first, uint32_t S, int32_t p, int32_t c,
+                                        unsigned long long rank) {
+  if ((uint32_t)p >= S || (uint32_t)c >= S) return;  // counted as ST_BADSVC by the table add
+  unsigned long long* f = &first[(size_t)p * S + (uint32_t)c];
+  if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > rank) atomicMin(f, rank);
+}
+__device__ __forceinline__ unsigned long long ord_rank(uint64_t trace_pos, uint32_t bfs, int k) {
+  return ((unsigned long long)trace_pos << 24) | ((unsigned long long)bfs << 1) | (unsigned long long)k;
 }
 
 // QueryRequest.test's time rule over a trace in storage order (QueryRequest.java:262-279):

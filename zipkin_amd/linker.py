@@ -9,8 +9,11 @@ throws, this raises: ReferenceNullPointerException for quirk Q1
 (Span.Builder.merge of a null endpoint), ReferenceIllegalArgumentException.
 
 Work runs in libzdl (include/zdl.h) on the GPU; there is no CPU path.
-Output order: the reference returns links in LinkedHashMap insertion order;
-this returns them sorted by (parent, child) in String order.
+Output order: like the reference, ``link()`` returns links in LinkedHashMap
+insertion order (first addLink over the traces in put order, each tree
+breadth-first; ZDL_FLAG_INSERTION_ORDER). With
+``insertion_order=False`` the engine takes its streaming path and ``link()``
+returns the same links sorted by (parent, child) in String order.
 ``merge`` keeps the reference's first-seen order.
 """
 from __future__ import annotations
@@ -34,8 +37,9 @@ def _capacity(n: int) -> int:
 
 
 class DependencyLinker:
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, insertion_order: bool = True):
         self.device = device
+        self.insertion_order = insertion_order
         self.svc = Dictionary()
         self.ip4 = Dictionary()
         self.ip6 = Dictionary()
@@ -46,13 +50,13 @@ class DependencyLinker:
     def _context(self) -> N.Context:
         need = _capacity(max(len(self.svc), 1))
         if self._ctx is None:
-            self._ctx = N.Context(need, self.device)
+            self._ctx = N.Context(need, self.device, insertion_order=self.insertion_order)
             self._ranked = (-1, -1, -1)
         elif self._ctx.n_services < need:
-            # grow the S x S table: carry the counts over on the device
-            p, c, n, e = self._ctx.link()
+            # grow the S x S table: carry the counts (in order) over on the device
+            p, c, n, e = self._ctx.link(self._order())
             old = self._ctx
-            self._ctx = N.Context(need, self.device)
+            self._ctx = N.Context(need, self.device, insertion_order=self.insertion_order)
             self._ranked = (-1, -1, -1)
             if len(p):
                 self._ctx.add_links(p, c, n, e)
@@ -64,6 +68,9 @@ class DependencyLinker:
             self._ctx.set_ranks(N.ZDL_DICT_IPV6, self.ip6.ranks())
             self._ranked = sizes
         return self._ctx
+
+    def _order(self) -> int:
+        return N.ZDL_ORDER_INSERTION if self.insertion_order else N.ZDL_ORDER_SORTED
 
     # -- reference API --------------------------------------------------------
     def put_trace(self, spans: Sequence[Span]) -> "DependencyLinker":
@@ -91,7 +98,7 @@ class DependencyLinker:
         """link() (DependencyLinker.java:184)."""
         if self._ctx is None:
             return []
-        p, c, n, e = self._ctx.link()
+        p, c, n, e = self._ctx.link(self._order())
         s = self.svc.strings
         return [DependencyLink.create(s[a], s[b], int(x), int(y)) for a, b, x, y in zip(p, c, n, e)]
 

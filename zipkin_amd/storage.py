@@ -110,7 +110,10 @@ class InMemoryStorage:
             to_recover -= len(victims)
 
     def _grouped(self) -> Columns:
-        """Alive spans grouped by trace_lo, IMS storage order inside each trace."""
+        """Alive spans grouped by trace_lo, in getDependencies' trace order: IMS iterates
+        spansByTraceIdTimeStamp in TIMESTAMP_DESCENDING order (timestamp, then lowTraceId,
+        both descending; IMS:272-291, 356-366), so a trace comes at its newest key. Inside a
+        trace: IMS storage order (spansByTraceId, IMS:448-454)."""
         cols = self._columns()
         idx = np.nonzero(self._alive)[0]
         if len(idx) == 0:
@@ -123,7 +126,11 @@ class InMemoryStorage:
         inv = inv.reshape(-1)
         first = np.full(inv.max() + 1, np.iinfo(np.int64).max, np.int64)
         np.minimum.at(first, inv, np.arange(len(idx), dtype=np.int64))
-        order = np.lexsort((np.arange(len(idx)), first[inv], low))
+        ulow, tinv = np.unique(low, return_inverse=True)
+        newest = np.full(len(ulow), np.iinfo(np.int64).min, np.int64)
+        np.maximum.at(newest, tinv.reshape(-1), ts)
+        newest = newest[tinv.reshape(-1)]
+        order = np.lexsort((np.arange(len(idx)), first[inv], ~low, -newest))
         sel = idx[order]
         low_sorted = cols.trace_lo[sel]
         starts = np.nonzero(np.concatenate([[True], low_sorted[1:] != low_sorted[:-1]]))[0]
