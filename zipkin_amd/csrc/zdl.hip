@@ -75,7 +75,8 @@ struct Args {
   unsigned long long* prof;  // ZDL_PROF=1: k_link phase cycles (12 counters)
   uint64_t* cx_win;      // k_link -> k_tail: (base | P << 48, starts mask) per window
   uint32_t skip;         // timing-only ablation of k_link (ZDL_SKIP): 32 stream only, 64 fields,
-                         // 128 +hash, 256 +parents, 512 +jumping, 2048 no table adds, 4096 cache-resident
+                         // 128 +hash, 256 +parents, 512 +jumping, 2048 no table adds, 4096 cache-resident;
+                         // k_tail insertion order: 8192 no breadth-first ranks, 16384 no ord_min
   // big-trace scratch (HBM), indexed by global span index
   uint64_t* b_id;
   uint64_t* b_pid;
@@ -921,7 +922,8 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   const int dense = SS <= (size_t)WDENSE_MAX;
   const int grid = c->grid, lgrid = c->cus * lk::wgs_per_cu;  // k_link: two 16-wave workgroups per CU
   HIP_TRY(c, c->big_list.ensure(n_traces));
-  HIP_TRY(c, c->cx_win.ensure(2 * std::min<uint64_t>(n_traces, n_spans)));
+  // queued windows: at most one per trace; mode 3 (insertion order) uses one slot per trace
+  HIP_TRY(c, c->cx_win.ensure(2 * (c->ord ? n_traces : std::min<uint64_t>(n_traces, n_spans))));
   Args A{};
   A.c = Cols{col->id, col->parent_id, col->local_svc, col->remote_svc, col->local_ip4, col->local_ip6,
              col->port_flags, col->timestamp};
