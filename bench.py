@@ -45,6 +45,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--cpu-sample-traces", type=int, default=200_000)
+    ap.add_argument("--no-insertion-order", action="store_true",
+                    help="skip the side measurement of the insertion-order mode (N = 1 only)")
     args = ap.parse_args()
 
     import torch
@@ -129,6 +131,28 @@ def main():
         total_spans = cols.n_spans
 
     p, c, n, e = out
+    # side measurement (not `value`): the same batch on an insertion-order context, whose
+    # link() is DependencyLinker.link()'s list order (k_link plans, k_tail links exactly)
+    ins = None
+    ins_out = None
+    if world == 1 and not args.no_insertion_order:
+        ictx = N.Context(S, device=local, insertion_order=True)
+
+        def istep():
+            ictx.reset()
+            ictx.put_spans_device(ptrs, cols.n_spans, doff.data_ptr(), cols.n_traces)
+            return ictx.link(N.ZDL_ORDER_INSERTION)
+
+        istep()
+        ictx.sync()
+        ik = 3
+        t1 = time.perf_counter()
+        for _ in range(ik):
+            ins_out = istep()
+        ictx.sync()
+        it = (time.perf_counter() - t1) / ik
+        ictx.close()
+        ins = {"ms_per_step": it * 1e3, "spans_per_s": cols.n_spans / it, "steps": ik, "parity": None}
     parity = None
     cpu = None
     if rank == 0 and world == 1 and not args.no_parity:
@@ -140,6 +164,12 @@ def main():
         got = sorted(zip(p.tolist(), c.tolist(), n.tolist(), e.tolist()))
         exp = sorted(zip(op.tolist(), oc.tolist(), on.tolist(), oe.tolist()))
         parity = "bit-exact" if (st == 0 and got == exp) else "MISMATCH"
+        if ins is not None:
+            ip, ic, inn, ie = ins_out
+            iseq = list(zip(ip.tolist(), ic.tolist(), inn.tolist(), ie.tolist()))
+            oseq = list(zip(op.tolist(), oc.tolist(), on.tolist(), oe.tolist()))
+            ins["parity"] = "exact order" if (st == 0 and iseq == oseq) else "MISMATCH"
+            log(f"insertion order: {ins['ms_per_step']:.2f} ms/step, {ins['parity']}")
         log(f"parity vs C++ restatement ({threads} threads, {t_multi:.2f}s): {parity}, {len(got)} links")
         if not args.no_cpu_baseline:
             k = min(args.cpu_sample_traces, cols.n_traces)
@@ -191,7 +221,7 @@ def main():
                        "services": S, "parallelism": f"trace-shard x{world}" + (" + RCCL all-reduce" if world > 1 else ""),
                        "kernel_ms": {"k_link": tiles},
                        "step_roofline_frac": bytes_path / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                       "parity": parity, "links": int(len(p))},
+                       "parity": parity, "links": int(len(p)), "insertion_order": ins},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "k_link", "algorithmic_bytes_per_launch": bytes_launch},
