@@ -193,6 +193,35 @@ int zdl_reset(zdl_ctx* ctx);
 int zdl_table_export(zdl_ctx* ctx, void* dev_call, void* dev_err);
 int zdl_table_import(zdl_ctx* ctx, const void* dev_call, const void* dev_err);
 
+/* ---- daily buckets (the zipkin-dependencies job; ITDependencies.aggregateLinks,
+ * zipkin/src/test/java/zipkin2/storage/ITDependencies.java:666-700) ----
+ * zdl_set_days: from now on every trace is linked into the bucket of its day - the
+ * flooredTraceTimestamp rule over its spans in storage order (:680-690), with `timestamp`
+ * holding guessTimestamp (Span.timestamp, else the first annotation's, :692-700) - for the
+ * n_days (<= 255) UTC days from day0_ms (a midnight). A trace without a timestamp or
+ * outside the range fails the put (ZDL_EINVAL). Resets the counts; n_days = 0 turns it off.
+ * Not with a time window. Tables hold n_days * S * S cells; zdl_table_export/import move
+ * all of them. zdl_link is refused while days are set: */
+int zdl_set_days(zdl_ctx* ctx, int64_t day0_ms, uint32_t n_days);
+
+typedef struct zdl_day_links {
+  uint64_t       n_days;
+  const int64_t* day_ms;       /* the days that hold a trace (with or without links):
+                                  ZDL_ORDER_INSERTION first-seen order, else ascending */
+  uint64_t       n;
+  const int64_t* day;          /* per link: its midnight (ms) */
+  const int32_t* parent;
+  const int32_t* child;
+  const int64_t* call_count;
+  const int64_t* error_count;
+} zdl_day_links;
+
+/* The per-day link lists: ZDL_ORDER_INSERTION = aggregateLinks' LinkedHashMap (days in
+ * the order their first trace was put, each day's links in DependencyLinker.link() order;
+ * needs ZDL_FLAG_INSERTION_ORDER), ZDL_ORDER_SORTED = by (day, parent, child). Owned by the
+ * context until the next link call. */
+int zdl_link_days(zdl_ctx* ctx, int order, zdl_day_links* out);
+
 /* Kernel durations of the most recent put (+ link) when ZDL_FLAG_TIMING is set. */
 int zdl_get_kernel_times(zdl_ctx* ctx, zdl_kernel_times* out);
 

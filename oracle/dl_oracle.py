@@ -538,6 +538,62 @@ class InMemoryStorage:
         return linker.link()
 
 
+# ------------------------------------------------- daily buckets (zipkin-dependencies)
+# zipkin/src/test/java/zipkin2/storage/ITDependencies.java:666-700,
+# storage/GroupByTraceId.java:41-54, internal/DateUtil.java:27-35.
+DAY_MS = 86_400_000
+
+
+def midnight_utc(epoch_millis: int) -> int:
+    """DateUtil.midnightUTC: the Calendar fields below the day zeroed (a floor)."""
+    return (epoch_millis // DAY_MS) * DAY_MS
+
+
+def _java_div(a: int, b: int) -> int:
+    """Java long division (truncates toward zero)."""
+    q = abs(a) // abs(b)
+    return q if (a >= 0) == (b >= 0) else -q
+
+
+def guess_timestamp(span: Span) -> int:
+    """ITDependencies.guessTimestamp (:692-700)."""
+    if span.timestamp != 0:
+        return span.timestamp
+    for ts, _ in span.annotations:
+        if 0 < ts:
+            return ts
+    return 0
+
+
+def floored_trace_timestamp(trace: List[Span]) -> int:
+    """ITDependencies.flooredTraceTimestamp (:680-690), literally: micros are compared
+    with the (already floored) millis of the current value."""
+    m = 2 ** 63 - 1
+    for span in trace:
+        current = guess_timestamp(span)
+        if current != 0 and current < m:
+            m = midnight_utc(_java_div(current, 1000))
+    assert m != 2 ** 63 - 1, "trace without a timestamp"
+    return m
+
+
+def group_by_trace_id(spans: Iterable[Span], strict: bool = False) -> List[List[Span]]:
+    """GroupByTraceId.map (:41-54): LinkedHashMap by (low) trace id."""
+    groups: Dict[str, List[Span]] = {}
+    for s in spans:
+        groups.setdefault(s.trace_id if strict else s.trace_lo, []).append(s)
+    return list(groups.values())
+
+
+def aggregate_links(spans: Iterable[Span]) -> Dict[int, List[DependencyLink]]:
+    """ITDependencies.aggregateLinks (:666-677): midnight -> DependencyLinker.link()."""
+    linkers: Dict[int, DependencyLinker] = {}
+    for trace in group_by_trace_id(spans, False):
+        midnight = floored_trace_timestamp(trace)
+        linkers.setdefault(midnight, DependencyLinker()).put_trace(trace)
+    return {m: l.link() for m, l in linkers.items()}
+
+
 @functools.total_ordering
 class _Desc:
     """Reverses java String order for the TIMESTAMP_DESCENDING tiebreak."""

@@ -1,0 +1,141 @@
+"""Daily-bucketed links: ITDependencies.aggregateLinks
+(zipkin/src/test/java/zipkin2/storage/ITDependencies.java:666-700).
+
+* CPU: the oracle's restatement (oracle/dl_oracle.py aggregate_links) is pinned by the
+  reference's own ITDependencies expectations: a store that keeps aggregateLinks' daily
+  links answers getDependencies(endTs, lookback) by merging the days DateUtil.getDays
+  names (internal/DateUtil.java:37-47) with DependencyLinker.merge - every transcribed
+  ITDependencies case must hold that way too.
+* GPU: zipkin_amd.daily.aggregate_links (zdl_set_days / zdl_link_days) against the oracle,
+  exact (days in first-seen order, each day's links in DependencyLinker.link() order),
+  and the raw context against per-day C++ restatement runs at larger sizes.
+"""
+import random
+
+import numpy as np
+import pytest
+
+from oracle import dl_oracle as O
+from tests.golden_io import check_links, load, spans
+from tests.stress import random_trace
+from zipkin_amd.model import Span
+
+ST = load("storage_dependencies.json")
+DAY = O.DAY_MS
+
+
+def get_days(end_ts, lookback):
+    """DateUtil.getDays (DateUtil.java:37-47), as midnights in ms."""
+    to = O.midnight_utc(end_ts)
+    start = end_ts - (lookback if lookback != 0 else end_ts)
+    frm = 0 if start <= 0 else O.midnight_utc(start)
+    return list(range(frm, to + 1, DAY))
+
+
+def _all_spans(case):
+    out = []
+    for b in case["batches"]:
+        out += spans(b)
+    return out
+
+
+@pytest.mark.parametrize("case", ST["cases"], ids=lambda c: c["name"] + "@" + c["ref"].split(":")[-1])
+def test_oracle_daily_pinned_by_itdependencies(case):
+    daily = O.aggregate_links(_all_spans(case))
+    for q in case["queries"]:
+        picked = [l for d in get_days(q["endTs"], q["lookback"]) for l in daily.get(d, [])]
+        check_links(O.DependencyLinker.merge(picked), q["expect"], "only")
+
+
+def test_oracle_floored_timestamp_quirk():
+    """flooredTraceTimestamp compares micros with the floored millis: only the first
+    timestamped span (storage order) decides, unless a later one is tiny."""
+    def sp(i, ts, ann=()):
+        return Span.create("a", format(i, "016x"), timestamp=ts, annotations=ann)
+    t = 1_700_000_000_000_000  # micros
+    assert O.floored_trace_timestamp([sp(1, 0), sp(2, t + DAY * 1000), sp(3, t)]) == \
+        O.midnight_utc((t + DAY * 1000) // 1000)
+    assert O.floored_trace_timestamp([sp(1, t), sp(2, 5_000_000)]) == 0  # 5 s after the epoch
+    assert O.floored_trace_timestamp([sp(1, 0, ((t, "cs"),))]) == O.midnight_utc(t // 1000)
+
+
+def _multi_day_spans(seed, n_traces=60, days=3):
+    r = random.Random(seed)
+    base = 1_704_067_200_000_000  # 2024-01-01 in micros
+    out = []
+    for k in range(n_traces):
+        t = random_trace(r, allow_npe=False)
+        tid = format(r.getrandbits(64) | 1, "016x")
+        day = r.randrange(days)
+        for s in t:
+            ts = base + day * DAY * 1000 + r.randrange(DAY * 1000)
+            ann = ()
+            if r.random() < 0.3:  # only an annotation carries the time (guessTimestamp)
+                ann, ts = ((ts, "sr"),), 0
+            out.append(s.to_builder(trace_id=tid, timestamp=ts, annotations=ann))
+    r.shuffle(out)  # GroupByTraceId keeps first-seen trace order and in-trace order
+    return out
+
+
+def _as_lists(d):
+    return [(day, [(l.parent, l.child, l.call_count, l.error_count) for l in ls]) for day, ls in d.items()]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(40))
+def test_gpu_daily_vs_oracle(seed):
+    from zipkin_amd.daily import aggregate_links
+    sp = _multi_day_spans(seed)
+    assert _as_lists(aggregate_links(sp)) == _as_lists(O.aggregate_links(sp))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", [c for c in ST["cases"] if c["batches"]], ids=lambda c: c["name"])
+def test_gpu_daily_golden_cases(case):
+    from zipkin_amd.daily import aggregate_links
+    sp = _all_spans(case)
+    assert _as_lists(aggregate_links(sp)) == _as_lists(O.aggregate_links(sp))
+
+
+@pytest.mark.gpu
+def test_gpu_daily_sorted_and_large_vs_cpp():
+    """C2-shaped batch spread over 4 days: each day's table equals the C++ restatement
+    run on that day's traces (sorted mode, streaming of the exact path)."""
+    from oracle import ref
+    from zipkin_amd import _native as N
+    from zipkin_amd import synth
+    from zipkin_amd.columnar import Columns
+    w = synth.C2.scaled(40_000)
+    cols = synth.generate(w)
+    r = np.random.default_rng(3)
+    off = cols.offsets.astype(np.int64)
+    day0 = (w.base_ts_us // 1000 // DAY) * DAY
+    tday = r.integers(0, 4, cols.n_traces)
+    ts = cols.timestamp.copy()
+    shift = np.repeat(tday, np.diff(off)) * DAY * 1000
+    ts = np.where(ts != 0, ts + shift, 0)
+    # every trace needs a timestamp: give the first span one where the trace has none
+    for t in range(cols.n_traces):
+        if off[t + 1] > off[t] and not ts[off[t]:off[t + 1]].any():
+            ts[off[t]] = w.base_ts_us + tday[t] * DAY * 1000
+    f = ("trace_lo", "id", "parent_id", "local_svc", "remote_svc", "local_ip4", "local_ip6", "port_flags")
+    c2 = Columns(*(getattr(cols, n) for n in f), np.ascontiguousarray(ts), cols.offsets)
+    ctx = N.Context(w.total_services)
+    ctx.set_days(day0, 6)
+    ctx.put_spans(c2)
+    days, day, p, c, n, e = ctx.link_days(N.ZDL_ORDER_SORTED)
+    ctx.close()
+    first_ts = np.array([ts[off[t]:off[t + 1]][ts[off[t]:off[t + 1]] != 0][0] for t in range(cols.n_traces)])
+    trace_day = (first_ts // 1000 // DAY) * DAY
+    for d in sorted(set(trace_day.tolist())):
+        sel = np.nonzero(trace_day == d)[0]
+        lens = off[sel + 1] - off[sel]
+        idx = np.concatenate([np.arange(off[t], off[t + 1]) for t in sel])
+        sub = Columns(*(np.ascontiguousarray(getattr(c2, n)[idx]) for n in f + ("timestamp",)),
+                      np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64))
+        st, op, oc, on, oe = ref.link(sub, threads=8)
+        assert st == 0
+        m = day == d
+        got = sorted(zip(p[m].tolist(), c[m].tolist(), n[m].tolist(), e[m].tolist()))
+        assert got == sorted(zip(op.tolist(), oc.tolist(), on.tolist(), oe.tolist()))
+    assert sorted(days.tolist()) == sorted(set(trace_day.tolist()))

@@ -30,7 +30,7 @@ EXPORTS = (
     "zdl_abi_version", "zdl_create", "zdl_create_error", "zdl_destroy", "zdl_last_error",
     "zdl_set_ranks", "zdl_set_window", "zdl_put_spans", "zdl_put_spans_device", "zdl_sync",
     "zdl_link", "zdl_merge_links", "zdl_add_links", "zdl_reset", "zdl_table_export",
-    "zdl_table_import", "zdl_get_kernel_times", "zdl_stream",
+    "zdl_table_import", "zdl_get_kernel_times", "zdl_stream", "zdl_set_days", "zdl_link_days",
 )
 
 
@@ -47,6 +47,12 @@ class Config(C.Structure):
 
 class Links(C.Structure):
     _fields_ = [("n", C.c_uint64), ("parent", C.POINTER(C.c_int32)), ("child", C.POINTER(C.c_int32)),
+                ("call_count", C.POINTER(C.c_int64)), ("error_count", C.POINTER(C.c_int64))]
+
+
+class DayLinks(C.Structure):
+    _fields_ = [("n_days", C.c_uint64), ("day_ms", C.POINTER(C.c_int64)), ("n", C.c_uint64),
+                ("day", C.POINTER(C.c_int64)), ("parent", C.POINTER(C.c_int32)), ("child", C.POINTER(C.c_int32)),
                 ("call_count", C.POINTER(C.c_int64)), ("error_count", C.POINTER(C.c_int64))]
 
 
@@ -100,11 +106,13 @@ def lib() -> C.CDLL:
     L.zdl_table_export.argtypes = [vp, vp, vp]
     L.zdl_table_import.argtypes = [vp, vp, vp]
     L.zdl_get_kernel_times.argtypes = [vp, C.POINTER(KernelTimes)]
+    L.zdl_set_days.argtypes = [vp, i64, u32]
+    L.zdl_link_days.argtypes = [vp, C.c_int, C.POINTER(DayLinks)]
     L.zdl_stream.restype = vp
     L.zdl_stream.argtypes = [vp]
     for name in ("zdl_set_ranks", "zdl_set_window", "zdl_put_spans", "zdl_put_spans_device", "zdl_sync",
                  "zdl_link", "zdl_merge_links", "zdl_add_links", "zdl_reset", "zdl_table_export",
-                 "zdl_table_import", "zdl_get_kernel_times"):
+                 "zdl_table_import", "zdl_get_kernel_times", "zdl_set_days", "zdl_link_days"):
         getattr(L, name).restype = C.c_int
     _lib = L
     return L
@@ -199,6 +207,22 @@ class Context:
         out = Links()
         self.check(self._L.zdl_link(self.h, int(order), C.byref(out)))
         return self._links_to_numpy(out)
+
+    def set_days(self, day0_ms: int, n_days: int):
+        """Daily buckets (zdl_set_days): the timestamp column then holds guessTimestamp."""
+        self.check(self._L.zdl_set_days(self.h, int(day0_ms), int(n_days)))
+
+    def link_days(self, order: int = ZDL_ORDER_SORTED):
+        """(days, day, parent, child, call, err): the days holding a trace, then per link."""
+        out = DayLinks()
+        self.check(self._L.zdl_link_days(self.h, int(order), C.byref(out)))
+        nd, n = int(out.n_days), int(out.n)
+        days = np.ctypeslib.as_array(out.day_ms, (nd,)).copy() if nd else np.zeros(0, np.int64)
+        if n == 0:
+            z32, z64 = np.zeros(0, np.int32), np.zeros(0, np.int64)
+            return days, z64, z32, z32.copy(), z64.copy(), z64.copy()
+        arr = lambda p: np.ctypeslib.as_array(p, (n,)).copy()  # noqa: E731
+        return days, arr(out.day), arr(out.parent), arr(out.child), arr(out.call_count), arr(out.error_count)
 
     def merge_links(self, parent, child, call, err):
         p, c = np.ascontiguousarray(parent, np.int32), np.ascontiguousarray(child, np.int32)

@@ -93,6 +93,12 @@ struct Args {
   // the put-global position of this put's span 0, and big-trace breadth-first scratch
   unsigned long long* first;
   uint64_t span_base;
+  // daily buckets (zdl_set_days): rows = days * S (else S), day 0 = midnight day0 (ms);
+  // day_first[d] = put-global position of day d's first trace
+  uint32_t rows;
+  uint32_t days;
+  int64_t day0;
+  unsigned long long* day_first;
   unsigned long long* o_key;
   uint32_t* o_fa;
   uint32_t* o_fb;
@@ -307,6 +313,35 @@ __device__ __forceinline__ void big_traces(const Args& A) {
       big_sync();
       if (!sh_act) { big_sync(); continue; }
     }
+    if (A.days) {  // daily buckets: flooredTraceTimestamp over the trace in storage order
+      if (threadIdx.x == 0) sh_ts_root_idx = 0x7fffffffffffffffll;
+      big_sync();
+      for (int s = threadIdx.x; s < n; s += BIG_WG)  // the first span with a timestamp
+        if (A.c.ts[b + s] != 0) atomicMin((long long*)&sh_ts_root_idx, (long long)s);
+      big_sync();
+      const int f0 = sh_ts_root_idx == 0x7fffffffffffffffll ? n : (int)sh_ts_root_idx;
+      const int64_t m1 = f0 < n ? floored_step(INT64_MAX, A.c.ts[b + f0]) : INT64_MAX;
+      if (threadIdx.x == 0) sh_act = 0;
+      big_sync();
+      // a later span changes m only if its micros compare below m's millis: find any
+      for (int s = f0 + 1 + threadIdx.x; s < n; s += BIG_WG)
+        if (A.c.ts[b + s] != 0 && A.c.ts[b + s] < m1) sh_act = 1;
+      big_sync();
+      if (threadIdx.x == 0) {
+        int64_t m = m1;
+        if (sh_act)  // the literal walk (never for real clocks)
+          for (int s = f0 + 1; s < n; ++s) m = floored_step(m, A.c.ts[b + s]);
+        sh_act = 1;
+        const int64_t d = m == INT64_MAX ? -1 : (m - A.day0) / DAY_MS;
+        const bool ok = m != INT64_MAX && m >= A.day0 && d < (int64_t)A.days;
+        if (!ok) atomicOr(A.status, ST_DAYS);
+        else ord_min(&A.day_first[d], A.span_base + b);
+        sh_ts_min = ok ? d : -1;
+      }
+      big_sync();
+      if (sh_ts_min < 0) { big_sync(); continue; }
+    }
+    const uint32_t day = A.days ? (uint32_t)sh_ts_min : 0u;
     // bitonic sort of perm by span_less (any n: out-of-range partners are +inf)
     int npad = 1;
     while (npad < n) npad <<= 1;
@@ -375,10 +410,10 @@ __device__ __forceinline__ void big_traces(const Args& A) {
       if (v.parent[p] == PAR_NONMEMBER) continue;
       link_node(v, p, rp, n, [&](int32_t a, int32_t c, bool e, int k) {
         if ((uint32_t)a >= A.S || (uint32_t)c >= A.S) { atomicOr(A.status, ST_BADSVC); return; }
-        const size_t idx = (size_t)a * A.S + c;
+        const size_t idx = ((size_t)day * A.S + (size_t)a) * A.S + c;  // row day * S + parent
         atomicAdd(&A.call[idx], 1ull);
         if (e) atomicAdd(&A.err[idx], 1ull);
-        if (ORD) ord_min(A.first, A.S, a, c, ord_rank(A.span_base + b, bfs[p], k));
+        if (ORD) ord_min(&A.first[idx], ord_rank(A.span_base + b, bfs[p], k));
       });
     }
     big_sync();
@@ -505,11 +540,15 @@ __global__ void __launch_bounds__(TAIL_WG, 1) k_tail(Args A) {
   if (threadIdx.x == 0) last = atomicAdd(A.done, 1u) == gridDim.x - 1;
   __syncthreads();
   if (!last) return;
-  compact_ordered(A.call, A.err, A.S * A.S, A.S, A.status, A.map);
+  compact_ordered(A.call, A.err, A.rows * A.S, A.S, A.status, A.map);
   if (threadIdx.x == 0) *A.done = 0;
 }
 
 inline const void* k_tail_fn(int dense, int window, int ord = 0) {
+  if (window == 2) {  // daily buckets
+    if (ord) return dense ? (const void*)k_tail<1, 2, 1> : (const void*)k_tail<0, 2, 1>;
+    return dense ? (const void*)k_tail<1, 2, 0> : (const void*)k_tail<0, 2, 0>;
+  }
   if (ord) {
     if (dense) return window ? (const void*)k_tail<1, 1, 1> : (const void*)k_tail<1, 0, 1>;
     return window ? (const void*)k_tail<0, 1, 1> : (const void*)k_tail<0, 0, 1>;
@@ -612,6 +651,12 @@ struct zdl_ctx {
   // insertion order (ZDL_FLAG_INSERTION_ORDER): first-addLink rank per cell, the put-global
   // position of the next put's span 0, big-trace breadth-first scratch
   bool ord = false;
+  // daily buckets (zdl_set_days): the tables hold rows = days * S parent rows
+  uint32_t days = 0, rows = 0;
+  int64_t day0 = 0;
+  DevBuf<unsigned long long> day_first;
+  std::vector<unsigned long long> h_day_first;
+  std::vector<int64_t> out_day, out_days;
   DevBuf<unsigned long long> first, o_key;
   uint64_t span_base = 0;
   DevBuf<uint32_t> o_fa, o_fb, o_bfs;
@@ -700,6 +745,7 @@ int status_code(zdl_ctx* c, uint32_t st) {
   if (st & ST_BADOFF) return fail(c, ZDL_EINVAL, "trace offsets are not non-decreasing");
   if (st & ST_INTERNAL) return fail(c, ZDL_EDEVICE, "internal consistency check failed on the device");
   if (st & ST_ORDLIM) return fail(c, ZDL_EINVAL, "insertion order: a trace has more than 2^21 - 2 spans");
+  if (st & ST_DAYS) return fail(c, ZDL_EINVAL, "daily buckets: a trace has no timestamp or its day is outside the range");
   return ZDL_OK;
 }
 
@@ -754,6 +800,7 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
   c->S = cfg->n_services;
   c->flags = cfg->flags;
   c->ord = (cfg->flags & ZDL_FLAG_INSERTION_ORDER) != 0;
+  c->rows = cfg->n_services;
   c->lk_stride = std::max<uint32_t>(1u, cfg->timing_stride);
   hipError_t e = hipSetDevice(c->device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
@@ -762,13 +809,13 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
   if (e == hipSuccess) e = c->errc.ensure(SS);
   if (e == hipSuccess) e = c->status.ensure(4);
   if (e == hipSuccess) e = c->count.ensure(1);
-  if (e == hipSuccess) e = hipMemset(c->call.p, 0, SS * 8);
-  if (e == hipSuccess) e = hipMemset(c->errc.p, 0, SS * 8);
-  if (e == hipSuccess) e = hipMemset(c->status.p, 0, 16);
+  if (e == hipSuccess) e = hipMemsetAsync(c->call.p, 0, SS * 8, c->stream);
+  if (e == hipSuccess) e = hipMemsetAsync(c->errc.p, 0, SS * 8, c->stream);
+  if (e == hipSuccess) e = hipMemsetAsync(c->status.p, 0, 16, c->stream);
   if (e == hipSuccess && c->ord) e = c->first.ensure(SS);
-  if (e == hipSuccess && c->ord) e = hipMemset(c->first.p, 0xff, SS * 8);
+  if (e == hipSuccess && c->ord) e = hipMemsetAsync(c->first.p, 0xff, SS * 8, c->stream);
   if (e == hipSuccess) e = c->counters.ensure(5);  // + k_tail's finished-workgroup count
-  if (e == hipSuccess) e = hipMemset(c->counters.p, 0, 20);
+  if (e == hipSuccess) e = hipMemsetAsync(c->counters.p, 0, 20, c->stream);
   if (e == hipSuccess) e = hipHostMalloc((void**)&c->h_meta, 16, hipHostMallocDefault);
   // timing-only events: no system-scope fence (cache writeback) between the kernels they bracket
   for (int i = 0; i < 8 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->ev[i], hipEventDisableSystemFence);
@@ -799,11 +846,15 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
     c->prof_on = pe && pe[0] == '1';
     if (c->prof_on) {
       e = c->prof.ensure(12);
-      if (e == hipSuccess) e = hipMemset(c->prof.p, 0, 12 * 8);
+      if (e == hipSuccess) e = hipMemsetAsync(c->prof.p, 0, 12 * 8, c->stream);
     }
     const char* sk = getenv("ZDL_SKIP");
     c->skip = sk ? (uint32_t)strtoul(sk, nullptr, 0) : 0u;
   }
+  // the initial memsets run on the context's (non-blocking) stream and are waited for
+  // here: a null-stream hipMemset is not ordered before the first put's kernels on a
+  // non-blocking stream, and could land after k_link had counted (lost big-trace lists)
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e != hipSuccess) {
     g_create_error = std::string("device init failed: ") + hipGetErrorString(e);
     zdl_destroy(c);
@@ -818,7 +869,7 @@ void zdl_destroy(zdl_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (auto& r : c->rank) r.release();
   c->call.release(); c->errc.release(); c->status.release();
-  c->first.release(); c->o_key.release(); c->o_fa.release(); c->o_fb.release(); c->o_bfs.release();
+  c->first.release(); c->day_first.release(); c->o_key.release(); c->o_fa.release(); c->o_fb.release(); c->o_bfs.release();
   c->big_list.release(); c->counters.release();
   c->cx_win.release();
   if (c->prof_on && c->prof.p) {
@@ -875,8 +926,30 @@ int zdl_set_ranks(zdl_ctx* c, int dict, const int32_t* rank, uint32_t n) {
   return ZDL_OK;
 }
 
+int zdl_set_days(zdl_ctx* c, int64_t day0_ms, uint32_t n_days) {
+  if (!c) return ZDL_EINVAL;
+  if (n_days > 255) return fail(c, ZDL_EINVAL, "zdl_set_days: at most 255 days");
+  if (n_days && (day0_ms % DAY_MS) != 0) return fail(c, ZDL_EINVAL, "zdl_set_days: day0 must be a UTC midnight");
+  if (n_days && c->window) return fail(c, ZDL_EINVAL, "zdl_set_days: not with a time window");
+  if ((uint64_t)(n_days ? n_days : 1) * c->S * c->S >= (1ull << 32))
+    return fail(c, ZDL_EINVAL, "zdl_set_days: days * S * S must stay below 2^32");
+  HIP_TRY(c, enter(c));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  c->days = n_days;
+  c->day0 = n_days ? day0_ms : 0;
+  c->rows = (n_days ? n_days : 1) * c->S;
+  const size_t SS = (size_t)c->rows * c->S;
+  HIP_TRY(c, c->call.ensure(SS));
+  HIP_TRY(c, c->errc.ensure(SS));
+  if (c->ord) HIP_TRY(c, c->first.ensure(SS));
+  if (n_days) HIP_TRY(c, c->day_first.ensure(n_days));
+  c->map_fresh = false;
+  return zdl_reset(c);
+}
+
 int zdl_set_window(zdl_ctx* c, int64_t end_ts_ms, int64_t lookback_ms) {
   if (!c) return ZDL_EINVAL;
+  if (c->days && lookback_ms > 0) return fail(c, ZDL_EINVAL, "zdl_set_window: not with daily buckets");
   if (lookback_ms <= 0) {
     c->window = 0;
     return ZDL_OK;
@@ -918,12 +991,12 @@ static hipError_t ensure_map(zdl_ctx* c) {
 // compacts the table into the mapped buffer zdl_link reads.
 static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans, const uint64_t* off,
                           uint64_t n_traces, const uint64_t* n_traces_dev = nullptr) {
-  const size_t SS = (size_t)c->S * c->S;
+  const size_t SS = (size_t)c->rows * c->S;  // table cells (days * S * S with daily buckets)
   const int dense = SS <= (size_t)WDENSE_MAX;
   const int grid = c->grid, lgrid = c->cus * lk::wgs_per_cu;  // k_link: two 16-wave workgroups per CU
   HIP_TRY(c, c->big_list.ensure(n_traces));
   // queued windows: at most one per trace; mode 3 (insertion order) uses one slot per trace
-  HIP_TRY(c, c->cx_win.ensure(2 * (c->ord ? n_traces : std::min<uint64_t>(n_traces, n_spans))));
+  HIP_TRY(c, c->cx_win.ensure(2 * ((c->ord || c->days) ? n_traces : std::min<uint64_t>(n_traces, n_spans))));
   Args A{};
   A.c = Cols{col->id, col->parent_id, col->local_svc, col->remote_svc, col->local_ip4, col->local_ip6,
              col->port_flags, col->timestamp};
@@ -936,6 +1009,11 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   A.S = c->S;
   A.dense = dense;
   A.window = c->window;
+  A.rows = c->rows;
+  A.days = c->days;
+  A.day0 = c->day0;
+  A.day_first = c->day_first.p;
+  const int wmode = c->days ? 2 : c->window;  // k_tail's timestamp mode
   A.win_lo = c->win_lo;
   A.win_hi = c->win_hi;
   A.call = c->call.p;
@@ -954,7 +1032,7 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   void* kargs[] = {&A};
   ev_record(c, 0);
   ev_record(c, 1);
-  const int lmode = c->ord ? 3 : (c->prof_on ? 1 : (c->skip ? 2 : 0));
+  const int lmode = (c->ord || c->days) ? 3 : (c->prof_on ? 1 : (c->skip ? 2 : 0));
   HIP_TRY(c, hipLaunchKernel(k_link_fn(dense, c->window, lmode), dim3(lgrid),
                              dim3(lk::waves(c->window) * 64), kargs, link_block_bytes(c->window), c->stream));
   ev_record(c, 7);
@@ -994,12 +1072,12 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
     A.o_fb = c->o_fb.p;
     A.o_bfs = c->o_bfs.p;
   }
-  const bool ordered = SS <= (size_t)COMPACT_WG * 8 && !c->ord;
+  const bool ordered = SS <= (size_t)COMPACT_WG * 8 && !c->ord && !c->days;
   if (ordered) HIP_TRY(c, ensure_map(c));
   A.map = ordered && !getenv("ZDL_NOTAILMAP") ? c->d_map : nullptr;
   A.done = c->counters.p + 4;
-  HIP_TRY(c, hipLaunchKernel(k_tail_fn(dense, c->window, c->ord ? 1 : 0), dim3(grid), dim3(TAIL_WG), kargs,
-                             tail_block_bytes(c->window), c->stream));
+  HIP_TRY(c, hipLaunchKernel(k_tail_fn(dense, wmode, c->ord ? 1 : 0), dim3(grid), dim3(TAIL_WG), kargs,
+                             tail_block_bytes(wmode), c->stream));
   c->span_base += n_spans;  // the next put's traces come after this one's
   ev_record(c, 4);
   ++c->epoch;  // k_tail zeroed the other counter slots
@@ -1021,12 +1099,13 @@ static int put_spans_ungrouped(zdl_ctx* c, const zdl_span_cols* col, uint64_t n)
   HIP_TRY(c, c->g_ip4.ensure(n));
   HIP_TRY(c, c->g_ip6.ensure(n));
   HIP_TRY(c, c->g_pf.ensure(n));
-  if (c->window) HIP_TRY(c, c->g_ts.ensure(n));
+  const bool with_ts = c->window || c->days;
+  if (with_ts) HIP_TRY(c, c->g_ts.ensure(n));
   const Cols in{col->id, col->parent_id, col->local_svc, col->remote_svc, col->local_ip4, col->local_ip6,
-                col->port_flags, c->window ? col->timestamp : nullptr};
+                col->port_flags, with_ts ? col->timestamp : nullptr};
   hipLaunchKernelGGL(k_gather, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, in, c->grp.perm, n,
                      c->g_id.p, c->g_pid.p, c->g_lsvc.p, c->g_rsvc.p, c->g_ip4.p, c->g_ip6.p, c->g_pf.p,
-                     c->window ? c->g_ts.p : nullptr);
+                     with_ts ? c->g_ts.p : nullptr);
   HIP_TRY(c, hipGetLastError());
   zdl_span_cols g{};
   g.id = c->g_id.p;
@@ -1036,7 +1115,7 @@ static int put_spans_ungrouped(zdl_ctx* c, const zdl_span_cols* col, uint64_t n)
   g.local_ip4 = c->g_ip4.p;
   g.local_ip6 = c->g_ip6.p;
   g.port_flags = c->g_pf.p;
-  g.timestamp = c->window ? c->g_ts.p : nullptr;
+  g.timestamp = with_ts ? c->g_ts.p : nullptr;
   return put_spans_link(c, &g, n, c->grp.off, n, c->grp.count);
 }
 
@@ -1047,7 +1126,8 @@ int zdl_put_spans_device(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans,
   if (!col->id || !col->parent_id || !col->local_svc || !col->remote_svc || !col->local_ip4 ||
       !col->local_ip6 || !col->port_flags)
     return fail(c, ZDL_EINVAL, "missing column");
-  if (c->window && !col->timestamp) return fail(c, ZDL_EINVAL, "window set but no timestamp column");
+  if ((c->window || c->days) && !col->timestamp)
+    return fail(c, ZDL_EINVAL, "window or days set but no timestamp column");
   if (n_traces >= 0xffffffffull || n_spans >= (1ull << 40)) return fail(c, ZDL_EINVAL, "input too large");
   HIP_TRY(c, enter(c));
   if (!off) return put_spans_ungrouped(c, col, n_spans);
@@ -1113,8 +1193,8 @@ int zdl_put_spans(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans, const 
   d.local_ip4 = c->h_ip4.p;
   d.local_ip6 = c->h_ip6.p;
   d.port_flags = c->h_pf.p;
-  if (c->window) {
-    if (!col->timestamp) return fail(c, ZDL_EINVAL, "window set but no timestamp column");
+  if (c->window || c->days) {
+    if (!col->timestamp) return fail(c, ZDL_EINVAL, "window or days set but no timestamp column");
     HIP_TRY(c, c->h_ts.ensure(n_spans));
     HIP_TRY(c, hipMemcpyAsync(c->h_ts.p, col->timestamp, n_spans * 8, hipMemcpyHostToDevice, s));
     d.timestamp = c->h_ts.p;
@@ -1127,10 +1207,11 @@ int zdl_put_spans(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans, const 
 int zdl_reset(zdl_ctx* c) {
   if (!c) return ZDL_EINVAL;
   HIP_TRY(c, enter(c));
-  const size_t SS = (size_t)c->S * c->S;
+  const size_t SS = (size_t)c->rows * c->S;
   hipLaunchKernelGGL(k_zero_tables, dim3((unsigned)((SS + 255) / 256)), dim3(256), 0, c->stream, c->call.p,
                      c->errc.p, (uint64_t)SS, c->status.p, c->ord ? c->first.p : nullptr);
   c->span_base = 0;
+  if (c->days) HIP_TRY(c, hipMemsetAsync(c->day_first.p, 0xff, (size_t)c->days * 8, c->stream));
   HIP_TRY(c, hipGetLastError());
   c->map_fresh = false;
   return ZDL_OK;  // stream-ordered: no host wait
@@ -1163,7 +1244,7 @@ static void sort_output(zdl_ctx* c, size_t n) {
 // zdl_link in ZDL_ORDER_INSERTION: the non-zero cells with their first-addLink ranks
 // (k_merge_compact over the context's tables), ordered by rank.
 static int link_insertion(zdl_ctx* c, zdl_links* out) {
-  const uint64_t SS = (uint64_t)c->S * c->S;
+  const uint64_t SS = (uint64_t)c->rows * c->S;
   HIP_TRY(c, c->o_p.ensure(SS));
   HIP_TRY(c, c->o_c.ensure(SS));
   HIP_TRY(c, c->o_call.ensure(SS));
@@ -1211,6 +1292,7 @@ static int link_insertion(zdl_ctx* c, zdl_links* out) {
 
 int zdl_link(zdl_ctx* c, int order, zdl_links* out) {
   if (!c || !out) return ZDL_EINVAL;
+  if (c->days) return fail(c, ZDL_EINVAL, "daily buckets are set: use zdl_link_days");
   if (order == ZDL_ORDER_INSERTION) {
     if (!c->ord) return fail(c, ZDL_EINVAL, "ZDL_ORDER_INSERTION needs a ZDL_FLAG_INSERTION_ORDER context");
     HIP_TRY(c, enter(c));
@@ -1298,6 +1380,110 @@ int zdl_link(zdl_ctx* c, int order, zdl_links* out) {
   return ZDL_OK;
 }
 
+// Daily buckets: the cells as (day, parent, child, counts), ordered like
+// ITDependencies.aggregateLinks' map of per-day DependencyLinker.link() lists.
+int zdl_link_days(zdl_ctx* c, int order, zdl_day_links* out) {
+  if (!c || !out) return ZDL_EINVAL;
+  if (!c->days) return fail(c, ZDL_EINVAL, "zdl_link_days: no daily buckets (zdl_set_days)");
+  if (order == ZDL_ORDER_INSERTION && !c->ord)
+    return fail(c, ZDL_EINVAL, "ZDL_ORDER_INSERTION needs a ZDL_FLAG_INSERTION_ORDER context");
+  if (order != ZDL_ORDER_INSERTION && order != ZDL_ORDER_SORTED)
+    return fail(c, ZDL_EINVAL, "zdl_link_days: order must be ZDL_ORDER_SORTED or ZDL_ORDER_INSERTION");
+  HIP_TRY(c, enter(c));
+  const uint64_t SS = (uint64_t)c->rows * c->S;
+  HIP_TRY(c, c->o_p.ensure(SS));
+  HIP_TRY(c, c->o_c.ensure(SS));
+  HIP_TRY(c, c->o_call.ensure(SS));
+  HIP_TRY(c, c->o_err.ensure(SS));
+  HIP_TRY(c, c->o_first.ensure(SS));
+  HIP_TRY(c, hipMemsetAsync(c->count.p, 0, 8, c->stream));
+  if (c->ord) {  // non-zero cells with their first-addLink ranks
+    hipLaunchKernelGGL(k_merge_compact, dim3((unsigned)((SS + 255) / 256)), dim3(256), 0, c->stream, c->call.p,
+                       c->errc.p, c->first.p, SS, c->S, c->count.p, c->o_p.p, c->o_c.p, c->o_call.p, c->o_err.p,
+                       c->o_first.p);
+  } else {
+    HIP_TRY(c, c->o_links.ensure(SS));
+    hipLaunchKernelGGL(k_compact, dim3((unsigned)((SS + 255) / 256)), dim3(256), 0, c->stream, c->call.p, c->errc.p,
+                       SS, c->S, c->count.p, c->o_links.p);
+  }
+  HIP_TRY(c, hipGetLastError());
+  unsigned long long m = 0;
+  HIP_TRY(c, hipMemcpyAsync(&m, c->count.p, 8, hipMemcpyDeviceToHost, c->stream));
+  c->h_day_first.assign(c->days, 0);
+  HIP_TRY(c, hipMemcpyAsync(c->h_day_first.data(), c->day_first.p, (size_t)c->days * 8, hipMemcpyDeviceToHost,
+                            c->stream));
+  const int rc = zdl_sync(c);
+  if (rc != ZDL_OK) return rc;
+  std::vector<int32_t> row(m), ch(m);
+  std::vector<int64_t> ca(m), er(m);
+  std::vector<uint64_t> first(m, 0);
+  if (m && c->ord) {
+    HIP_TRY(c, hipMemcpy(row.data(), c->o_p.p, m * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(c, hipMemcpy(ch.data(), c->o_c.p, m * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(c, hipMemcpy(ca.data(), c->o_call.p, m * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(c, hipMemcpy(er.data(), c->o_err.p, m * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(c, hipMemcpy(first.data(), c->o_first.p, m * 8, hipMemcpyDeviceToHost));
+  } else if (m) {
+    std::vector<ZLink> recs(m);
+    HIP_TRY(c, hipMemcpy(recs.data(), c->o_links.p, m * sizeof(ZLink), hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < m; ++i) {
+      row[i] = recs[i].parent;
+      ch[i] = recs[i].child;
+      ca[i] = recs[i].call;
+      er[i] = recs[i].err;
+    }
+  }
+  const std::vector<int32_t>& r = c->host_rank[0];
+  auto rk = [&](int32_t id) -> int64_t { return (size_t)id < r.size() ? r[id] : id; };
+  const uint32_t S = c->S;
+  std::vector<uint32_t> idx(m);
+  for (size_t i = 0; i < m; ++i) idx[i] = (uint32_t)i;
+  if (order == ZDL_ORDER_INSERTION) {  // days by first trace, then the day's linker order
+    std::sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) {
+      const uint64_t fa = c->h_day_first[(uint32_t)row[a] / S], fb = c->h_day_first[(uint32_t)row[b] / S];
+      if (fa != fb) return fa < fb;
+      return first[a] < first[b];
+    });
+  } else {  // (day, parent, child) with names in String order
+    std::sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) {
+      const uint32_t da = (uint32_t)row[a] / S, db = (uint32_t)row[b] / S;
+      if (da != db) return da < db;
+      const int64_t pa = rk(row[a] % (int32_t)S), pb = rk(row[b] % (int32_t)S);
+      if (pa != pb) return pa < pb;
+      return rk(ch[a]) < rk(ch[b]);
+    });
+  }
+  c->out_day.resize(m);
+  c->out_p.resize(m);
+  c->out_c.resize(m);
+  c->out_call.resize(m);
+  c->out_err.resize(m);
+  for (size_t i = 0; i < m; ++i) {
+    const uint32_t j = idx[i];
+    c->out_day[i] = c->day0 + (int64_t)((uint32_t)row[j] / S) * DAY_MS;
+    c->out_p[i] = (int32_t)((uint32_t)row[j] % S);
+    c->out_c[i] = ch[j];
+    c->out_call[i] = ca[j];
+    c->out_err[i] = er[j];
+  }
+  std::vector<uint32_t> dl;  // the days that hold a trace (links or not)
+  for (uint32_t d = 0; d < c->days; ++d)
+    if (c->h_day_first[d] != ~0ull) dl.push_back(d);
+  if (order == ZDL_ORDER_INSERTION)
+    std::sort(dl.begin(), dl.end(), [&](uint32_t a, uint32_t b) { return c->h_day_first[a] < c->h_day_first[b]; });
+  c->out_days.resize(dl.size());
+  for (size_t i = 0; i < dl.size(); ++i) c->out_days[i] = c->day0 + (int64_t)dl[i] * DAY_MS;
+  out->n_days = dl.size();
+  out->day_ms = c->out_days.data();
+  out->n = m;
+  out->day = c->out_day.data();
+  out->parent = c->out_p.data();
+  out->child = c->out_c.data();
+  out->call_count = c->out_call.data();
+  out->error_count = c->out_err.data();
+  return ZDL_OK;
+}
+
 int zdl_merge_links(zdl_ctx* c, const int32_t* parent, const int32_t* child, const int64_t* call_count,
                     const int64_t* error_count, uint64_t n, zdl_links* out) {
   if (!c || !out) return ZDL_EINVAL;
@@ -1376,6 +1562,7 @@ int zdl_merge_links(zdl_ctx* c, const int32_t* parent, const int32_t* child, con
 int zdl_add_links(zdl_ctx* c, const int32_t* parent, const int32_t* child, const int64_t* call_count,
                   const int64_t* error_count, uint64_t n) {
   if (!c) return ZDL_EINVAL;
+  if (c->days) return fail(c, ZDL_EINVAL, "zdl_add_links: not with daily buckets");
   if (n == 0) return ZDL_OK;
   HIP_TRY(c, enter(c));
   const uint64_t SS = (uint64_t)c->S * c->S;
@@ -1401,7 +1588,7 @@ int zdl_add_links(zdl_ctx* c, const int32_t* parent, const int32_t* child, const
 int zdl_table_export(zdl_ctx* c, void* dev_call, void* dev_err) {
   if (!c || !dev_call || !dev_err) return ZDL_EINVAL;
   HIP_TRY(c, enter(c));
-  const size_t bytes = (size_t)c->S * c->S * 8;
+  const size_t bytes = (size_t)c->rows * c->S * 8;
   HIP_TRY(c, hipMemcpyAsync(dev_call, c->call.p, bytes, hipMemcpyDeviceToDevice, c->stream));
   HIP_TRY(c, hipMemcpyAsync(dev_err, c->errc.p, bytes, hipMemcpyDeviceToDevice, c->stream));
   return ZDL_OK;
@@ -1411,7 +1598,7 @@ int zdl_table_import(zdl_ctx* c, const void* dev_call, const void* dev_err) {
   if (!c || !dev_call || !dev_err) return ZDL_EINVAL;
   if (c->ord) return fail(c, ZDL_EINVAL, "zdl_table_import: the table carries no insertion-order ranks");
   HIP_TRY(c, enter(c));
-  const size_t bytes = (size_t)c->S * c->S * 8;
+  const size_t bytes = (size_t)c->rows * c->S * 8;
   HIP_TRY(c, hipMemcpyAsync(c->call.p, dev_call, bytes, hipMemcpyDeviceToDevice, c->stream));
   HIP_TRY(c, hipMemcpyAsync(c->errc.p, dev_err, bytes, hipMemcpyDeviceToDevice, c->stream));
   c->map_fresh = false;

@@ -21,7 +21,7 @@
 
 namespace zdl {
 
-enum : uint32_t { ST_NPE = 1u, ST_BADSVC = 2u, ST_BADOFF = 4u, ST_IAE = 8u, ST_INTERNAL = 16u, ST_ORDLIM = 32u };
+enum : uint32_t { ST_NPE = 1u, ST_BADSVC = 2u, ST_BADOFF = 4u, ST_IAE = 8u, ST_INTERNAL = 16u, ST_ORDLIM = 32u, ST_DAYS = 64u };
 enum : int32_t { PAR_TERMINAL = -1, PAR_NONMEMBER = -3 };
 
 template <class PermT, class ParT>
@@ -378,14 +378,26 @@ __device__ __forceinline__ void link_node(const V& v, int p, int rp, int n, Emit
 // addLink of that (parent, child): (put-global position of the trace's first span) << 24
 // | (breadth-first index of the node << 1 | k). The plain load skips the atomic once a
 // smaller rank is in (ranks only decrease; a stale read only costs the atomic).
-__device__ __forceinline__ void ord_min(unsigned long long* first, uint32_t S, int32_t p, int32_t c,
-                                        unsigned long long rank) {
-  if ((uint32_t)p >= S || (uint32_t)c >= S) return;  // counted as ST_BADSVC by the table add
-  unsigned long long* f = &first[(size_t)p * S + (uint32_t)c];
+__device__ __forceinline__ void ord_min(unsigned long long* f, unsigned long long rank) {
   if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > rank) atomicMin(f, rank);
 }
 __device__ __forceinline__ unsigned long long ord_rank(uint64_t trace_pos, uint32_t bfs, int k) {
   return ((unsigned long long)trace_pos << 24) | ((unsigned long long)bfs << 1) | (unsigned long long)k;
+}
+
+// Daily buckets (ITDependencies.aggregateLinks, ITDependencies.java:666-700): a trace's day
+// is flooredTraceTimestamp's, restated literally over its spans in storage order: the first
+// span with a timestamp sets m = midnightUTC(ts / 1000) (Java long division, then
+// DateUtil.midnightUTC's floor, DateUtil.java:27-35); a later one replaces it only if its
+// microseconds compare below m's milliseconds (the reference's unit mix; never for real
+// clocks). INT64_MAX: no timestamp (the reference's assertion fails).
+constexpr int64_t DAY_MS = 86400000ll;
+__device__ __forceinline__ int64_t midnight_utc(int64_t ms) {
+  const int64_t q = ms / DAY_MS;
+  return (q - ((ms % DAY_MS) < 0 ? 1 : 0)) * DAY_MS;
+}
+__device__ __forceinline__ int64_t floored_step(int64_t m, int64_t ts) {
+  return (ts != 0 && ts < m) ? midnight_utc(ts / 1000) : m;
 }
 
 // QueryRequest.test's time rule over a trace in storage order (QueryRequest.java:262-279):
