@@ -161,6 +161,24 @@ int zdl_put_spans(zdl_ctx* ctx, const zdl_span_cols* cols, uint64_t n_spans,
 int zdl_put_spans_device(zdl_ctx* ctx, const zdl_span_cols* dev_cols, uint64_t n_spans,
                          const uint64_t* dev_trace_offsets, uint64_t n_traces);
 
+/* ---- device-resident span store (the ingest side of InMemoryStorage,
+ * storage/InMemoryStorage.java:156-181 accept) ----
+ * Spans are appended to HBM columns once (zdl_store_append copies the borrowed host
+ * columns; `timestamp` may be NULL = absent). A getDependencies-style query then uploads only
+ * its selection: zdl_put_stored links the stored spans perm[0..n_sel) as CSR-grouped traces
+ * (trace t = positions [trace_offsets[t], trace_offsets[t+1]) of perm, storage order), like
+ * zdl_put_spans would on the gathered columns. Synchronous. The store may serve any context
+ * of its device; eviction is the caller's (a selection simply leaves spans out). */
+typedef struct zdl_store zdl_store;
+zdl_store*  zdl_store_create(int device);
+void        zdl_store_destroy(zdl_store* store);
+const char* zdl_store_last_error(const zdl_store* store);
+int         zdl_store_append(zdl_store* store, const zdl_span_cols* cols, uint64_t n_spans);
+int         zdl_store_clear(zdl_store* store);
+uint64_t    zdl_store_size(const zdl_store* store);
+int zdl_put_stored(zdl_ctx* ctx, const zdl_store* store, const uint32_t* perm, uint64_t n_sel,
+                   const uint64_t* trace_offsets, uint64_t n_traces);
+
 /* Waits for the context stream and reports device-side status (e.g. ZDL_EREF_NPE). */
 int zdl_sync(zdl_ctx* ctx);
 

@@ -31,6 +31,8 @@ EXPORTS = (
     "zdl_set_ranks", "zdl_set_window", "zdl_put_spans", "zdl_put_spans_device", "zdl_sync",
     "zdl_link", "zdl_merge_links", "zdl_add_links", "zdl_reset", "zdl_table_export",
     "zdl_table_import", "zdl_get_kernel_times", "zdl_stream", "zdl_set_days", "zdl_link_days",
+    "zdl_store_create", "zdl_store_destroy", "zdl_store_last_error", "zdl_store_append", "zdl_store_clear",
+    "zdl_store_size", "zdl_put_stored",
 )
 
 
@@ -108,6 +110,19 @@ def lib() -> C.CDLL:
     L.zdl_get_kernel_times.argtypes = [vp, C.POINTER(KernelTimes)]
     L.zdl_set_days.argtypes = [vp, i64, u32]
     L.zdl_link_days.argtypes = [vp, C.c_int, C.POINTER(DayLinks)]
+    L.zdl_store_create.restype = vp
+    L.zdl_store_create.argtypes = [C.c_int]
+    L.zdl_store_destroy.argtypes = [vp]
+    L.zdl_store_last_error.restype = C.c_char_p
+    L.zdl_store_last_error.argtypes = [vp]
+    L.zdl_store_append.argtypes = [vp, C.POINTER(SpanCols), u64]
+    L.zdl_store_append.restype = C.c_int
+    L.zdl_store_clear.argtypes = [vp]
+    L.zdl_store_clear.restype = C.c_int
+    L.zdl_store_size.argtypes = [vp]
+    L.zdl_store_size.restype = u64
+    L.zdl_put_stored.argtypes = [vp, vp, vp, u64, vp, u64]
+    L.zdl_put_stored.restype = C.c_int
     L.zdl_stream.restype = vp
     L.zdl_stream.argtypes = [vp]
     for name in ("zdl_set_ranks", "zdl_set_window", "zdl_put_spans", "zdl_put_spans_device", "zdl_sync",
@@ -224,6 +239,12 @@ class Context:
         arr = lambda p: np.ctypeslib.as_array(p, (n,)).copy()  # noqa: E731
         return days, arr(out.day), arr(out.parent), arr(out.child), arr(out.call_count), arr(out.error_count)
 
+    def put_stored(self, store: "Store", perm: np.ndarray, offsets: np.ndarray) -> None:
+        """zdl_put_stored: link stored spans perm[...] as CSR traces (offsets over perm)."""
+        pm = np.ascontiguousarray(perm, np.uint32)
+        off = np.ascontiguousarray(offsets, np.uint64)
+        self.check(self._L.zdl_put_stored(self.h, store.h, _ptr(pm), len(pm), _ptr(off), len(off) - 1))
+
     def merge_links(self, parent, child, call, err):
         p, c = np.ascontiguousarray(parent, np.int32), np.ascontiguousarray(child, np.int32)
         n, e = np.ascontiguousarray(call, np.int64), np.ascontiguousarray(err, np.int64)
@@ -252,3 +273,39 @@ class Context:
 
     def stream(self) -> int:
         return self._L.zdl_stream(self.h) or 0
+
+
+class Store:
+    """zdl_store: span columns resident in HBM, appended once per accept."""
+
+    def __init__(self, device: int = 0):
+        L = lib()
+        h = L.zdl_store_create(int(device))
+        if not h:
+            raise ZdlError(ZDL_EDEVICE, L.zdl_create_error().decode())
+        self.h = C.c_void_p(h)
+        self._L = L
+
+    def append(self, cols) -> None:
+        sc = SpanCols(None, _ptr(cols.id), _ptr(cols.parent_id), _ptr(cols.local_svc), _ptr(cols.remote_svc),
+                      _ptr(cols.local_ip4), _ptr(cols.local_ip6), _ptr(cols.port_flags), _ptr(cols.timestamp))
+        rc = self._L.zdl_store_append(self.h, C.byref(sc), cols.n_spans)
+        if rc != ZDL_OK:
+            raise ZdlError(rc, self._L.zdl_store_last_error(self.h).decode())
+
+    def clear(self) -> None:
+        self._L.zdl_store_clear(self.h)
+
+    def __len__(self) -> int:
+        return int(self._L.zdl_store_size(self.h))
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._L.zdl_store_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

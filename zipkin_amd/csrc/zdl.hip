@@ -1119,6 +1119,162 @@ static int put_spans_ungrouped(zdl_ctx* c, const zdl_span_cols* col, uint64_t n)
   return put_spans_link(c, &g, n, c->grp.off, n, c->grp.count);
 }
 
+// ------------------------------------------------------------------ span store
+// A device-resident column store (the ingest side of InMemoryStorage):
+// accepted spans are appended to HBM columns once; a query uploads only the selection
+// (a u32 permutation in storage order + CSR offsets) and gathers on the device.
+struct zdl_store {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  uint64_t n = 0, cap = 0;
+  DevBuf<uint64_t> id, pid;
+  DevBuf<int32_t> lsvc, rsvc, ip4, ip6;
+  DevBuf<uint32_t> pf;
+  DevBuf<int64_t> ts;
+};
+
+}  // extern "C"
+namespace {
+template <class T>
+hipError_t store_grow(DevBuf<T>& b, uint64_t keep, uint64_t cap, hipStream_t s) {
+  DevBuf<T> nb;
+  hipError_t e = nb.ensure(cap);
+  if (e == hipSuccess && keep) e = hipMemcpyAsync(nb.p, b.p, keep * sizeof(T), hipMemcpyDeviceToDevice, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    nb.release();
+    return e;
+  }
+  b.release();
+  b = nb;
+  return hipSuccess;
+}
+int store_fail(zdl_store* st, int code, const std::string& msg) {
+  if (st) st->err = msg;
+  return code;
+}
+}  // namespace
+extern "C" {
+
+zdl_store* zdl_store_create(int device) {
+  zdl_store* st = new zdl_store();
+  st->device = device;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&st->stream, hipStreamNonBlocking) != hipSuccess) {
+    g_create_error = "zdl_store_create: device init failed";
+    delete st;
+    return nullptr;
+  }
+  return st;
+}
+
+void zdl_store_destroy(zdl_store* st) {
+  if (!st) return;
+  (void)hipSetDevice(st->device);
+  (void)hipStreamSynchronize(st->stream);
+  st->id.release(); st->pid.release(); st->lsvc.release(); st->rsvc.release(); st->ip4.release();
+  st->ip6.release(); st->pf.release(); st->ts.release();
+  (void)hipStreamDestroy(st->stream);
+  delete st;
+}
+
+const char* zdl_store_last_error(const zdl_store* st) { return st ? st->err.c_str() : "null store"; }
+
+uint64_t zdl_store_size(const zdl_store* st) { return st ? st->n : 0; }
+
+int zdl_store_clear(zdl_store* st) {
+  if (!st) return ZDL_EINVAL;
+  st->n = 0;
+  return ZDL_OK;
+}
+
+int zdl_store_append(zdl_store* st, const zdl_span_cols* col, uint64_t n) {
+  if (!st || !col) return ZDL_EINVAL;
+  if (n == 0) return ZDL_OK;
+  if (!col->id || !col->parent_id || !col->local_svc || !col->remote_svc || !col->local_ip4 || !col->local_ip6 ||
+      !col->port_flags)
+    return store_fail(st, ZDL_EINVAL, "zdl_store_append: missing column");
+  if (st->n + n >= (1ull << 32)) return store_fail(st, ZDL_EINVAL, "zdl_store_append: store limited to 2^32 spans");
+  (void)hipGetLastError();
+  hipError_t e = hipSetDevice(st->device);
+  const hipStream_t s = st->stream;
+  if (e == hipSuccess && st->n + n > st->cap) {  // grow by doubling (HBM is large; appends stay O(1))
+    const uint64_t cap = std::max<uint64_t>(st->n + n, std::max<uint64_t>(2 * st->cap, 1 << 16));
+    if (e == hipSuccess) e = store_grow(st->id, st->n, cap, s);
+    if (e == hipSuccess) e = store_grow(st->pid, st->n, cap, s);
+    if (e == hipSuccess) e = store_grow(st->lsvc, st->n, cap, s);
+    if (e == hipSuccess) e = store_grow(st->rsvc, st->n, cap, s);
+    if (e == hipSuccess) e = store_grow(st->ip4, st->n, cap, s);
+    if (e == hipSuccess) e = store_grow(st->ip6, st->n, cap, s);
+    if (e == hipSuccess) e = store_grow(st->pf, st->n, cap, s);
+    if (e == hipSuccess) e = store_grow(st->ts, st->n, cap, s);
+    if (e == hipSuccess) st->cap = cap;
+  }
+  const uint64_t o = st->n;
+  if (e == hipSuccess) e = hipMemcpyAsync(st->id.p + o, col->id, n * 8, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(st->pid.p + o, col->parent_id, n * 8, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(st->lsvc.p + o, col->local_svc, n * 4, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(st->rsvc.p + o, col->remote_svc, n * 4, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(st->ip4.p + o, col->local_ip4, n * 4, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(st->ip6.p + o, col->local_ip6, n * 4, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(st->pf.p + o, col->port_flags, n * 4, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess)
+    e = col->timestamp ? hipMemcpyAsync(st->ts.p + o, col->timestamp, n * 8, hipMemcpyHostToDevice, s)
+                       : hipMemsetAsync(st->ts.p + o, 0, n * 8, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);  // the columns are borrowed for the call only
+  if (e != hipSuccess)
+    return store_fail(st, e == hipErrorOutOfMemory ? ZDL_ENOMEM : ZDL_EDEVICE,
+                      std::string("zdl_store_append: ") + hipGetErrorString(e));
+  st->n += n;
+  return ZDL_OK;
+}
+
+int zdl_put_stored(zdl_ctx* c, const zdl_store* st, const uint32_t* perm, uint64_t n_sel, const uint64_t* off,
+                   uint64_t n_traces) {
+  if (!c || !st || (n_sel && !perm) || !off) return fail(c, ZDL_EINVAL, "null argument");
+  if (st->device != c->device) return fail(c, ZDL_EINVAL, "zdl_put_stored: store and context on different devices");
+  if (n_traces == 0 || n_sel == 0) return ZDL_OK;
+  if (off[0] != 0 || off[n_traces] != n_sel) return fail(c, ZDL_EINVAL, "trace offsets must span [0, n_sel]");
+  for (uint64_t t = 0; t < n_traces; ++t)
+    if (off[t + 1] < off[t]) return fail(c, ZDL_EINVAL, "trace offsets are not non-decreasing");
+  for (uint64_t i = 0; i < n_sel; ++i)
+    if (perm[i] >= st->n) return fail(c, ZDL_EINVAL, "zdl_put_stored: selection outside the store");
+  HIP_TRY(c, enter(c));
+  HIP_TRY(c, hipStreamSynchronize(st->stream));
+  const hipStream_t s = c->stream;
+  HIP_TRY(c, c->h_ord.ensure(n_sel));
+  HIP_TRY(c, c->h_off.ensure(n_traces + 1));
+  HIP_TRY(c, hipMemcpyAsync(c->h_ord.p, perm, n_sel * 4, hipMemcpyHostToDevice, s));
+  HIP_TRY(c, hipMemcpyAsync(c->h_off.p, off, (n_traces + 1) * 8, hipMemcpyHostToDevice, s));
+  HIP_TRY(c, c->g_id.ensure(n_sel));
+  HIP_TRY(c, c->g_pid.ensure(n_sel));
+  HIP_TRY(c, c->g_lsvc.ensure(n_sel));
+  HIP_TRY(c, c->g_rsvc.ensure(n_sel));
+  HIP_TRY(c, c->g_ip4.ensure(n_sel));
+  HIP_TRY(c, c->g_ip6.ensure(n_sel));
+  HIP_TRY(c, c->g_pf.ensure(n_sel));
+  const bool with_ts = c->window || c->days;
+  if (with_ts) HIP_TRY(c, c->g_ts.ensure(n_sel));
+  const Cols in{st->id.p, st->pid.p, st->lsvc.p, st->rsvc.p, st->ip4.p, st->ip6.p, st->pf.p,
+                with_ts ? st->ts.p : nullptr};
+  hipLaunchKernelGGL(k_gather, dim3((unsigned)((n_sel + 255) / 256)), dim3(256), 0, s, in, c->h_ord.p, n_sel,
+                     c->g_id.p, c->g_pid.p, c->g_lsvc.p, c->g_rsvc.p, c->g_ip4.p, c->g_ip6.p, c->g_pf.p,
+                     with_ts ? c->g_ts.p : nullptr);
+  HIP_TRY(c, hipGetLastError());
+  zdl_span_cols g{};
+  g.id = c->g_id.p;
+  g.parent_id = c->g_pid.p;
+  g.local_svc = c->g_lsvc.p;
+  g.remote_svc = c->g_rsvc.p;
+  g.local_ip4 = c->g_ip4.p;
+  g.local_ip6 = c->g_ip6.p;
+  g.port_flags = c->g_pf.p;
+  g.timestamp = with_ts ? c->g_ts.p : nullptr;
+  const int rc = put_spans_link(c, &g, n_sel, c->h_off.p, n_traces);
+  if (rc != ZDL_OK) return rc;
+  return zdl_sync(c);
+}
+
 int zdl_put_spans_device(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans, const uint64_t* off,
                          uint64_t n_traces) {
   if (!c || !col) return fail(c, ZDL_EINVAL, "null argument");

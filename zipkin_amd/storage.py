@@ -6,12 +6,14 @@ SpanStore.getDependencies(endTs, lookback) exercises:
 
 * builder flags strictTraceId / searchEnabled / maxSpanCount (IMS:72-100);
 * ``accept(spans)`` appends in arrival order and evicts the oldest traces past
-  maxSpanCount (IMS:156-211); spans are packed to columns on arrival;
+  maxSpanCount (IMS:156-211); spans are packed to columns on arrival and appended to a
+  device-resident store (zdl_store, HBM) once;
 * ``getDependencies(endTs, lookback)`` groups by the low 64 bits of the trace id
   (IMS:323-332, 448-467; strictTraceId is ignored here like the reference), keeps
   the storage order inside a trace (distinct (lowTraceId, timestamp) keys in
-  first-seen order, then insertion order), and hands the CSR-grouped columns to
-  the engine with the QueryRequest.test time window (QueryRequest.java:262-279)
+  first-seen order, then insertion order), and hands the engine only the selection
+  (a permutation of the stored spans + CSR offsets: zdl_put_stored gathers on the
+  device) with the QueryRequest.test time window (QueryRequest.java:262-279)
   evaluated on the device. Returns a single-use Call (Call.java:370-381).
 """
 from __future__ import annotations
@@ -20,7 +22,8 @@ from typing import Callable, Generic, List, Optional, Sequence, TypeVar
 
 import numpy as np
 
-from .columnar import Columns, concat_columns, pack_traces
+from . import _native as N
+from .columnar import pack_traces
 from .linker import DependencyLinker
 from .model import DependencyLink, Span
 
@@ -29,6 +32,11 @@ T = TypeVar("T")
 
 class IllegalStateException(RuntimeError):
     pass
+
+
+class NoSuchElementException(LookupError):
+    """What IMS.deleteOldestTrace throws when a batch alone exceeds maxSpanCount
+    (TreeMap.lastKey on an empty map, IMS:193-195)."""
 
 
 class Call(Generic[T]):
@@ -49,6 +57,11 @@ class Call(Generic[T]):
 
 
 class InMemoryStorage:
+    """The span columns live in HBM (a zdl_store, appended once per accept); the host keeps
+    only what eviction and trace order need (low trace id, timestamp, alive). A query
+    uploads its selection - a u32 permutation in getDependencies' order + CSR offsets - and
+    the device gathers and links (zdl_put_stored)."""
+
     def __init__(self, strict_trace_id: bool = True, search_enabled: bool = True,
                  max_span_count: int = 500000, device: int = 0):
         if max_span_count <= 0:
@@ -58,8 +71,9 @@ class InMemoryStorage:
         self.max_span_count = max_span_count
         self.device = device
         self._linker = DependencyLinker(device)  # owns the dictionaries
-        self._chunks: List[Columns] = []
-        self._cols: Optional[Columns] = None
+        self._store: Optional[N.Store] = None
+        self._lo = np.zeros(0, np.uint64)
+        self._ts = np.zeros(0, np.int64)
         self._alive = np.zeros(0, bool)
 
     @staticmethod
@@ -67,13 +81,6 @@ class InMemoryStorage:
         return _Builder()
 
     newBuilder = new_builder
-
-    def _columns(self) -> Columns:
-        if self._chunks:
-            parts = ([self._cols] if self._cols is not None else []) + self._chunks
-            self._cols = concat_columns(parts)
-            self._chunks = []
-        return self._cols
 
     def accept(self, spans: Sequence[Span]) -> Call[None]:
         spans = list(spans)
@@ -85,7 +92,11 @@ class InMemoryStorage:
             self._evict((n_now + len(spans)) - self.max_span_count)
             # one "trace" per span: grouping happens at query time
             cols = pack_traces([[s] for s in spans], self._linker.svc, self._linker.ip4, self._linker.ip6)
-            self._chunks.append(cols)
+            if self._store is None:
+                self._store = N.Store(self.device)
+            self._store.append(cols)
+            self._lo = np.concatenate([self._lo, cols.trace_lo])
+            self._ts = np.concatenate([self._ts, cols.timestamp])
             self._alive = np.concatenate([self._alive, np.ones(len(spans), bool)])
             return None
 
@@ -96,30 +107,29 @@ class InMemoryStorage:
     def _evict(self, to_recover: int):
         """deleteOldestTrace (IMS:193-211): the last key of TIMESTAMP_DESCENDING is the
         smallest timestamp, ties broken by the smallest lowTraceId."""
-        if to_recover <= 0:
-            return
-        cols = self._columns()
-        while to_recover > 0 and self._alive.any():
+        while to_recover > 0:
+            if not self._alive.any():
+                raise NoSuchElementException("evicting from an empty store")
             idx = np.nonzero(self._alive)[0]
-            ts = cols.timestamp[idx]
+            ts = self._ts[idx]
             m = ts.min()
             cand = idx[ts == m]
-            low = cols.trace_lo[cand].min()
-            victims = idx[cols.trace_lo[idx] == low]
+            low = self._lo[cand].min()
+            victims = idx[self._lo[idx] == low]
             self._alive[victims] = False
             to_recover -= len(victims)
 
-    def _grouped(self) -> Columns:
+    def _selection(self):
         """Alive spans grouped by trace_lo, in getDependencies' trace order: IMS iterates
         spansByTraceIdTimeStamp in TIMESTAMP_DESCENDING order (timestamp, then lowTraceId,
         both descending; IMS:272-291, 356-366), so a trace comes at its newest key. Inside a
-        trace: IMS storage order (spansByTraceId, IMS:448-454)."""
-        cols = self._columns()
+        trace: IMS storage order (spansByTraceId, IMS:448-454). Returns (store positions,
+        CSR offsets) or None."""
         idx = np.nonzero(self._alive)[0]
         if len(idx) == 0:
             return None
-        low = cols.trace_lo[idx]
-        ts = cols.timestamp[idx]
+        low = self._lo[idx]
+        ts = self._ts[idx]
         # first arrival index of each distinct (lowTraceId, timestamp) key
         keys = np.stack([low, ts.view(np.uint64)], axis=1)
         _, inv = np.unique(keys, axis=0, return_inverse=True)
@@ -132,13 +142,10 @@ class InMemoryStorage:
         newest = newest[tinv.reshape(-1)]
         order = np.lexsort((np.arange(len(idx)), first[inv], ~low, -newest))
         sel = idx[order]
-        low_sorted = cols.trace_lo[sel]
+        low_sorted = self._lo[sel]
         starts = np.nonzero(np.concatenate([[True], low_sorted[1:] != low_sorted[:-1]]))[0]
         offsets = np.concatenate([starts, [len(sel)]]).astype(np.uint64)
-        pick = lambda a: np.ascontiguousarray(a[sel])  # noqa: E731
-        return Columns(pick(cols.trace_lo), pick(cols.id), pick(cols.parent_id), pick(cols.local_svc),
-                       pick(cols.remote_svc), pick(cols.local_ip4), pick(cols.local_ip6),
-                       pick(cols.port_flags), pick(cols.timestamp), offsets)
+        return sel.astype(np.uint32), offsets
 
     def get_dependencies(self, end_ts: int, lookback: int) -> Call[List[DependencyLink]]:
         """SpanStore.getDependencies (SpanStore.java:85; IMS:323-332). Milliseconds."""
@@ -150,15 +157,16 @@ class InMemoryStorage:
         def run():
             if not self.search_enabled:
                 return []
-            grouped = self._grouped()
-            if grouped is None:
+            picked = self._selection()
+            if picked is None:
                 return []
+            sel, offsets = picked
             linker = DependencyLinker(self.device)
             linker.svc, linker.ip4, linker.ip6 = self._linker.svc, self._linker.ip4, self._linker.ip6
             try:
                 ctx = linker._context()
                 ctx.set_window(end_ts, lookback)
-                linker.put_columns(grouped)
+                ctx.put_stored(self._store, sel, offsets)
                 return linker.link()
             finally:
                 linker.close()
@@ -168,7 +176,17 @@ class InMemoryStorage:
     getDependencies = get_dependencies
 
     def clear(self):
-        self._chunks, self._cols, self._alive = [], None, np.zeros(0, bool)
+        if self._store is not None:
+            self._store.clear()
+        self._lo = np.zeros(0, np.uint64)
+        self._ts = np.zeros(0, np.int64)
+        self._alive = np.zeros(0, bool)
+
+    def close(self):
+        self._linker.close()
+        if self._store is not None:
+            self._store.close()
+            self._store = None
 
 
 class _Builder:
