@@ -72,6 +72,8 @@ struct Args {
   unsigned long long* map;   // mapped pinned host buffer: k_tail's last workgroup writes the
                              // ordered link records there (S*S <= 8192), else nullptr
   uint32_t* done;            // k_tail workgroups finished (the last one compacts; resets it)
+  unsigned long long* flag;  // mapped pinned: k_tail's last workgroup stores `seq` after the
+  unsigned long long seq;    // records (system-scope release), so zdl_link can spin on it
   unsigned long long* prof;  // ZDL_PROF=1: k_link phase cycles (12 counters)
   uint64_t* cx_win;      // k_link -> k_tail: (base | P << 48, starts mask) per window
   uint32_t skip;         // timing-only ablation of k_link (ZDL_SKIP): 32 stream only, 64 fields,
@@ -541,7 +543,12 @@ __global__ void __launch_bounds__(TAIL_WG, 1) k_tail(Args A) {
   __syncthreads();
   if (!last) return;
   compact_ordered(A.call, A.err, A.rows * A.S, A.S, A.status, A.map);
-  if (threadIdx.x == 0) *A.done = 0;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    *A.done = 0;
+    __threadfence_system();  // the records and counts are visible to the host before the flag
+    __hip_atomic_store(A.flag, A.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 inline const void* k_tail_fn(int dense, int window, int ord = 0) {
@@ -691,6 +698,9 @@ struct zdl_ctx {
   unsigned long long* h_map = nullptr;  // mapped pinned: status, count, ordered records
   unsigned long long* d_map = nullptr;  // its device address
   bool map_fresh = false;               // h_map holds the compaction of the current table
+  unsigned long long* h_flag = nullptr;  // mapped pinned: the last put's k_tail stores its seq
+  unsigned long long* d_flag = nullptr;
+  unsigned long long seq = 0;            // puts that compacted into h_map
   ZLink* h_links = nullptr;    // pinned link records
   size_t h_links_cap = 0;
   DevBuf<uint64_t> o_first;
@@ -896,6 +906,7 @@ void zdl_destroy(zdl_ctx* c) {
   c->o_links.release();
   if (c->h_meta) (void)hipHostFree(c->h_meta);
   if (c->h_map) (void)hipHostFree(c->h_map);
+  if (c->h_flag) (void)hipHostFree(c->h_flag);
   if (c->h_links) (void)hipHostFree(c->h_links);
   c->mi_p.release(); c->mi_c.release(); c->mi_call.release(); c->mi_err.release();
   for (auto& ev : c->ev)
@@ -983,6 +994,9 @@ static hipError_t ensure_map(zdl_ctx* c) {
   if (c->h_map) return hipSuccess;
   hipError_t e = hipHostMalloc((void**)&c->h_map, MAP_BYTES, hipHostMallocMapped | hipHostMallocCoherent);
   if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&c->d_map, c->h_map, 0);
+  if (e == hipSuccess) e = hipHostMalloc((void**)&c->h_flag, 64, hipHostMallocMapped | hipHostMallocCoherent);
+  if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&c->d_flag, c->h_flag, 0);
+  if (e == hipSuccess) *c->h_flag = 0;
   return e;
 }
 
@@ -1076,6 +1090,10 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   if (ordered) HIP_TRY(c, ensure_map(c));
   A.map = ordered && !getenv("ZDL_NOTAILMAP") ? c->d_map : nullptr;
   A.done = c->counters.p + 4;
+  if (A.map) {
+    A.flag = c->d_flag;
+    A.seq = ++c->seq;
+  }
   HIP_TRY(c, hipLaunchKernel(k_tail_fn(dense, wmode, c->ord ? 1 : 0), dim3(grid), dim3(TAIL_WG), kargs,
                              tail_block_bytes(wmode), c->stream));
   c->span_base += n_spans;  // the next put's traces come after this one's
@@ -1466,6 +1484,7 @@ int zdl_link(zdl_ctx* c, int order, zdl_links* out) {
     // status, count and records land in mapped pinned memory: written by the last put's
     // k_tail, or here when the table changed since
     HIP_TRY(c, ensure_map(c));
+    const bool tail_compacted = c->map_fresh;
     if (!c->map_fresh) {
       hipLaunchKernelGGL(k_compact_ordered, dim3(1), dim3(COMPACT_WG), 0, c->stream, c->call.p, c->errc.p,
                          (uint32_t)SS, c->S, c->status.p, c->d_map);
@@ -1473,7 +1492,21 @@ int zdl_link(zdl_ctx* c, int order, zdl_links* out) {
       c->map_fresh = true;
     }
     ev_record(c, 6);
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    // the last put's k_tail compacted: spin on its flag in mapped memory (a blocking
+    // stream sync costs ~10 us of host wake-up), checking the stream now and then so a
+    // failed kernel still surfaces; otherwise (or with every-kernel timing) a plain sync
+    bool seen = false;
+    if (!tail_compacted || ev_on(c, 6)) {
+      HIP_TRY(c, hipStreamSynchronize(c->stream));
+    } else {
+      const volatile unsigned long long* f = c->h_flag;
+      for (uint32_t i = 1;; ++i) {
+        if (*f == c->seq) { seen = true; break; }
+        if ((i & 255) == 0 && hipStreamQuery(c->stream) != hipErrorNotReady) break;
+        __builtin_ia32_pause();
+      }
+      if (!seen || *f != c->seq) HIP_TRY(c, hipStreamSynchronize(c->stream));  // surfaces a failure
+    }
     put_times(c);
     c->times.compact_ms = ev_ms(c, 5, 6);
     const int rc = status_code(c, (uint32_t)c->h_map[0]);
