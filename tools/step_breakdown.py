@@ -22,6 +22,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--config", default="c2")
+    ap.add_argument("--traces", type=int, default=0)
     a = ap.parse_args()
     import torch
 
@@ -29,6 +30,8 @@ def main():
     from zipkin_amd import synth
 
     w = synth.CONFIGS[a.config]
+    if a.traces:
+        w = w.scaled(a.traces)
     cols = synth.generate(w)
     dev = torch.device("cuda", 0)
     names = ("id", "parent_id", "local_svc", "remote_svc", "local_ip4", "local_ip6", "port_flags", "timestamp")

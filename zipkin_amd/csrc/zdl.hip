@@ -31,7 +31,7 @@ namespace zdl {
 
 constexpr int BIG_WG = 1024;        // threads per big-trace workgroup
 constexpr int HCAP = 2048;          // LDS hash slots of the (parent, child) table when S*S is large
-constexpr int HPROBE = 64;
+constexpr int HPROBE = 4;   // LDS hash probes before an add goes straight to HBM
 constexpr int WSMALL = 64;          // traces up to this many spans are k_link's
 constexpr int TAIL_WG = 1024;       // threads per k_tail workgroup (= BIG_WG)
 constexpr int WDENSE_MAX = 2560;    // S*S <= this -> dense u64 LDS cells (call | err << 32)
@@ -685,6 +685,7 @@ struct zdl_ctx {
   DevBuf<uint64_t> h_lo;
   // ungrouped input: zdl_group's sort + the columns in grouped order
   GroupWork grp;
+  LinkWork lw;  // zdl_link's device compaction for S * S > 8192
   DevBuf<uint64_t> g_id, g_pid;
   DevBuf<int32_t> g_lsvc, g_rsvc, g_ip4, g_ip6;
   DevBuf<uint32_t> g_pf;
@@ -898,7 +899,7 @@ void zdl_destroy(zdl_ctx* c) {
   c->b_hasc.release();
   c->h_id.release(); c->h_pid.release(); c->h_off.release(); c->h_lsvc.release(); c->h_rsvc.release();
   c->h_ip4.release(); c->h_ip6.release(); c->h_pf.release(); c->h_ts.release();
-  c->h_lo.release(); c->h_ord.release(); c->grp.release();
+  c->h_lo.release(); c->h_ord.release(); c->grp.release(); c->lw.release();
   c->g_id.release(); c->g_pid.release(); c->g_lsvc.release(); c->g_rsvc.release(); c->g_ip4.release();
   c->g_ip6.release(); c->g_pf.release(); c->g_ts.release();
   c->count.release(); c->m_call.release(); c->m_err.release(); c->m_first.release();
@@ -1478,7 +1479,6 @@ int zdl_link(zdl_ctx* c, int order, zdl_links* out) {
   const bool ordered = SS <= (uint64_t)COMPACT_WG * 8;
   ev_record(c, 5);
   size_t n = 0;
-  const ZLink* recs = nullptr;
   c->out_p.clear();
   if (ordered) {
     // status, count and records land in mapped pinned memory: written by the last put's
@@ -1518,49 +1518,35 @@ int zdl_link(zdl_ctx* c, int order, zdl_links* out) {
     c->out_call.assign(m.call, m.call + n);
     c->out_err.assign(m.err, m.err + n);
   } else {
-    // the record count lands next to the status word: status[0] status, status[2..3] count
-    unsigned long long* cnt = reinterpret_cast<unsigned long long*>(c->status.p + 2);
-    HIP_TRY(c, c->o_links.ensure(SS));
-    HIP_TRY(c, hipMemsetAsync(cnt, 0, 8, c->stream));
-    hipLaunchKernelGGL(k_compact, dim3((unsigned)((SS + 255) / 256)), dim3(256), 0, c->stream, c->call.p, c->errc.p,
-                       SS, c->S, cnt, c->o_links.p);
-    HIP_TRY(c, hipGetLastError());
+    // non-zero cells selected and (with ranks) radix-sorted on the device, in output order
+    HIP_TRY(c, c->o_p.ensure(SS));
+    HIP_TRY(c, c->o_c.ensure(SS));
+    HIP_TRY(c, c->o_call.ensure(SS));
+    HIP_TRY(c, c->o_err.ensure(SS));
+    uint64_t m = 0;
+    HIP_TRY(c, compact_links(c->lw, c->call.p, c->errc.p, SS, c->S, c->nrank[0] ? c->rank[0].p : nullptr,
+                             c->nrank[0], c->o_p.p, c->o_c.p, c->o_call.p, c->o_err.p, &m, c->stream));
     ev_record(c, 6);
-    // one round trip for the count and the status word, one for the records
+    c->out_p.resize(m);
+    c->out_c.resize(m);
+    c->out_call.resize(m);
+    c->out_err.resize(m);
     HIP_TRY(c, hipMemcpyAsync(c->h_meta, c->status.p, 16, hipMemcpyDeviceToHost, c->stream));
+    if (m) {
+      HIP_TRY(c, hipMemcpyAsync(c->out_p.data(), c->o_p.p, m * 4, hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(c, hipMemcpyAsync(c->out_c.data(), c->o_c.p, m * 4, hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(c, hipMemcpyAsync(c->out_call.data(), c->o_call.p, m * 8, hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(c, hipMemcpyAsync(c->out_err.data(), c->o_err.p, m * 8, hipMemcpyDeviceToHost, c->stream));
+    }
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     put_times(c);
     c->times.compact_ms = ev_ms(c, 5, 6);
     const int rc = status_code(c, (uint32_t)c->h_meta[0]);
     if (rc != ZDL_OK) return rc;
-    n = (size_t)c->h_meta[1];
-    if (n > c->h_links_cap) {
-      if (c->h_links) (void)hipHostFree(c->h_links);
-      c->h_links = nullptr;
-      c->h_links_cap = 0;
-      HIP_TRY(c, hipHostMalloc((void**)&c->h_links, n * sizeof(ZLink), hipHostMallocDefault));
-      c->h_links_cap = n;
-    }
-    if (n) {
-      HIP_TRY(c, hipMemcpyAsync(c->h_links, c->o_links.p, n * sizeof(ZLink), hipMemcpyDeviceToHost, c->stream));
-      HIP_TRY(c, hipStreamSynchronize(c->stream));
-    }
-    recs = c->h_links;
-  }
-  if (recs) {
-    c->out_p.resize(n);
-    c->out_c.resize(n);
-    c->out_call.resize(n);
-    c->out_err.resize(n);
-    for (size_t i = 0; i < n; ++i) {
-      c->out_p[i] = recs[i].parent;
-      c->out_c[i] = recs[i].child;
-      c->out_call[i] = recs[i].call;
-      c->out_err[i] = recs[i].err;
-    }
+    n = (size_t)m;
   }
   // cell order is (parent id, child id) order; names order needs the service rank table
-  if (!ordered || c->nrank[0] != 0) sort_output(c, n);
+  if (ordered && c->nrank[0] != 0) sort_output(c, n);  // the large path came sorted
   out->n = n;
   out->parent = c->out_p.data();
   out->child = c->out_c.data();

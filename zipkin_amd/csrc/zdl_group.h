@@ -31,4 +31,21 @@ struct GroupWork {
 hipError_t group_spans(GroupWork& g, const uint64_t* trace_lo, const uint32_t* ord, uint64_t n,
                        hipStream_t s);
 
+// The non-zero cells of an S x S count table as link records, on the device, in output
+// order: cell order (= (parent id, child id)), or by (rank[parent], rank[child]) when a rank
+// table is given (a stable 32-bit radix sort; ids past the table rank as themselves).
+// Replaces an atomic-counter compaction plus a host sort (7 ms at 250 000 links).
+struct LinkWork {
+  void* tmp = nullptr;
+  size_t tmp_bytes = 0;
+  uint32_t* sel[2] = {};
+  uint32_t* keys[2] = {};
+  uint64_t* count = nullptr;
+  size_t cap = 0;
+  void release();
+};
+hipError_t compact_links(LinkWork& w, const unsigned long long* call, const unsigned long long* err, uint64_t SS,
+                         uint32_t S, const int32_t* rank, uint32_t nrank, int32_t* parent, int32_t* child,
+                         int64_t* call_out, int64_t* err_out, uint64_t* n_out, hipStream_t s);
+
 }  // namespace zdl

@@ -113,4 +113,92 @@ hipError_t group_spans(GroupWork& g, const uint64_t* trace_lo, const uint32_t* o
   return hipGetLastError();
 }
 
+namespace {
+struct NonZeroCell {
+  const unsigned long long* call;
+  __host__ __device__ bool operator()(const uint32_t& i) const { return call[i] != 0; }
+};
+
+__device__ __forceinline__ uint32_t rank16(int32_t id, const int32_t* rank, uint32_t nrank) {
+  return (uint32_t)((uint32_t)id < nrank ? rank[id] : id) & 0xFFFFu;
+}
+
+__global__ void k_link_keys(const uint32_t* __restrict__ sel, const uint64_t* __restrict__ count, uint32_t S,
+                            const int32_t* __restrict__ rank, uint32_t nrank, uint32_t* __restrict__ keys) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= *count) return;
+  const uint32_t i = sel[j];
+  keys[j] = (rank16((int32_t)(i / S), rank, nrank) << 16) | rank16((int32_t)(i % S), rank, nrank);
+}
+
+__global__ void k_link_records(const uint32_t* __restrict__ sel, const uint64_t* __restrict__ count, uint32_t S,
+                               const unsigned long long* __restrict__ call, const unsigned long long* __restrict__ err,
+                               int32_t* __restrict__ p, int32_t* __restrict__ c, int64_t* __restrict__ n,
+                               int64_t* __restrict__ e) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= *count) return;
+  const uint32_t i = sel[j];
+  p[j] = (int32_t)(i / S);
+  c[j] = (int32_t)(i % S);
+  n[j] = (int64_t)call[i];
+  e[j] = (int64_t)err[i];
+}
+}  // namespace
+
+void LinkWork::release() {
+  for (auto*& q : sel) { if (q) (void)hipFree(q); q = nullptr; }
+  for (auto*& q : keys) { if (q) (void)hipFree(q); q = nullptr; }
+  if (count) (void)hipFree(count);
+  if (tmp) (void)hipFree(tmp);
+  count = nullptr;
+  tmp = nullptr;
+  tmp_bytes = 0;
+  cap = 0;
+}
+
+hipError_t compact_links(LinkWork& w, const unsigned long long* call, const unsigned long long* err, uint64_t SS,
+                         uint32_t S, const int32_t* rank, uint32_t nrank, int32_t* parent, int32_t* child,
+                         int64_t* call_out, int64_t* err_out, uint64_t* n_out, hipStream_t s) {
+  if (SS == 0 || SS >= (1ull << 32)) return hipErrorInvalidValue;
+  if (SS > w.cap) {
+    for (int b = 0; b < 2; ++b) {
+      GTRY(grow(w.sel[b], SS));
+      GTRY(grow(w.keys[b], SS));
+    }
+    if (!w.count) GTRY(hipMalloc((void**)&w.count, sizeof(uint64_t)));
+    size_t a = 0, b = 0;
+    GTRY(hipcub::DeviceSelect::If(nullptr, a, hipcub::CountingInputIterator<uint32_t>(0), w.sel[0], w.count, (int)SS,
+                                  NonZeroCell{call}, s));
+    GTRY(hipcub::DeviceRadixSort::SortPairs(nullptr, b, w.keys[0], w.keys[1], w.sel[0], w.sel[1], (int)SS, 0, 32, s));
+    const size_t need = std::max(a, b);
+    if (need > w.tmp_bytes) {
+      if (w.tmp) (void)hipFree(w.tmp);
+      w.tmp = nullptr;
+      w.tmp_bytes = 0;
+      GTRY(hipMalloc(&w.tmp, need));
+      w.tmp_bytes = need;
+    }
+    w.cap = SS;
+  }
+  size_t bytes = w.tmp_bytes;
+  GTRY(hipcub::DeviceSelect::If(w.tmp, bytes, hipcub::CountingInputIterator<uint32_t>(0), w.sel[0], w.count, (int)SS,
+                                NonZeroCell{call}, s));
+  uint64_t m = 0;
+  GTRY(hipMemcpyAsync(&m, w.count, 8, hipMemcpyDeviceToHost, s));
+  GTRY(hipStreamSynchronize(s));
+  *n_out = m;
+  if (m == 0) return hipSuccess;
+  const uint32_t* sel = w.sel[0];
+  if (rank) {
+    hipLaunchKernelGGL(k_link_keys, blocks(m), dim3(256), 0, s, w.sel[0], w.count, S, rank, nrank, w.keys[0]);
+    GTRY(hipGetLastError());
+    bytes = w.tmp_bytes;
+    GTRY(hipcub::DeviceRadixSort::SortPairs(w.tmp, bytes, w.keys[0], w.keys[1], w.sel[0], w.sel[1], (int)m, 0, 32, s));
+    sel = w.sel[1];
+  }
+  hipLaunchKernelGGL(k_link_records, blocks(m), dim3(256), 0, s, sel, w.count, S, call, err, parent, child,
+                     call_out, err_out);
+  return hipGetLastError();
+}
+
 }  // namespace zdl
