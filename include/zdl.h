@@ -163,8 +163,8 @@ int zdl_put_spans_device(zdl_ctx* ctx, const zdl_span_cols* dev_cols, uint64_t n
 
 /* ---- device-resident span store (the ingest side of InMemoryStorage,
  * storage/InMemoryStorage.java:156-181 accept) ----
- * Spans are appended to HBM columns once (zdl_store_append copies the borrowed host
- * columns; `timestamp` may be NULL = absent). A getDependencies-style query then uploads only
+ * Spans are appended to HBM columns once (zdl_store_append copies the borrowed columns, host
+ * or device memory, e.g. a zdl_decoded's; `timestamp` may be NULL = absent). A getDependencies-style query then uploads only
  * its selection: zdl_put_stored links the stored spans perm[0..n_sel) as CSR-grouped traces
  * (trace t = positions [trace_offsets[t], trace_offsets[t+1]) of perm, storage order), like
  * zdl_put_spans would on the gathered columns. Synchronous. The store may serve any context
@@ -239,6 +239,40 @@ typedef struct zdl_day_links {
  * needs ZDL_FLAG_INSERTION_ORDER), ZDL_ORDER_SORTED = by (day, parent, child). Owned by the
  * context until the next link call. */
 int zdl_link_days(zdl_ctx* ctx, int order, zdl_day_links* out);
+
+/* ---- proto3 ingest: SpanBytesDecoder.PROTO3.decodeList(bytes)
+ * (codec/SpanBytesDecoder.java:144-152, internal/Proto3Codec.java readList,
+ * internal/Proto3ZipkinFields.java:309-369) decoded on the device straight to span columns.
+ * Strings map to dictionary ids by the decoder's table of RAW keys: service names as the
+ * field's UTF-8 bytes before toLowerCase, ipv4 as 4 bytes, ipv6 as 16 bytes (after
+ * Endpoint.Builder.parseIp(byte[]), Endpoint.java:179-198). A decode that meets keys the
+ * table lacks returns ZDL_OK with n_missing > 0 and no columns: the caller assigns ids
+ * (lower-cased name -> its dictionary, first-seen order; zdl_decoder_missing lists the keys
+ * in (span, slot) order: local service, local ipv4, local ipv6, remote service), binds them
+ * and calls zdl_decode_proto3_retry, which re-runs on the resident batch.
+ * Status: ZDL_EREF_IAE where the reference throws IllegalArgumentException; ZDL_EINVAL for
+ * input the reference reads leniently across a message end (not supported). An empty
+ * input or a zero-length span message gives n_spans = 0 (the reference's empty list). */
+typedef struct zdl_decoder zdl_decoder;
+typedef struct zdl_decoded {
+  uint64_t        n_spans;
+  zdl_span_cols   dev;        /* device columns owned by the decoder (ord NULL), valid until
+                                 the next decode; feed zdl_put_spans_device / zdl_store_append */
+  const uint64_t* trace_lo;   /* host copies (owned by the decoder) for the storage facade */
+  const int64_t*  timestamp;
+  uint64_t        n_missing;  /* > 0: bind the keys, then zdl_decode_proto3_retry */
+} zdl_decoded;
+zdl_decoder* zdl_decoder_create(int device);
+void         zdl_decoder_destroy(zdl_decoder* dec);
+const char*  zdl_decoder_last_error(const zdl_decoder* dec);
+int          zdl_decoder_bind(zdl_decoder* dec, int dict, const uint8_t* key, uint32_t len, int32_t id);
+uint64_t     zdl_decoder_dict_size(const zdl_decoder* dec);
+int          zdl_decoder_missing(const zdl_decoder* dec, uint64_t i, int* dict, const uint8_t** key,
+                                 uint32_t* len);
+int          zdl_decode_proto3(zdl_decoder* dec, const uint8_t* bytes, uint64_t len, zdl_decoded* out);
+int          zdl_decode_proto3_retry(zdl_decoder* dec, zdl_decoded* out);
+/* copies the last decode's device columns into the non-NULL host columns of dst */
+int          zdl_decoder_download(zdl_decoder* dec, const zdl_span_cols* dst);
 
 /* Kernel durations of the most recent put (+ link) when ZDL_FLAG_TIMING is set. */
 int zdl_get_kernel_times(zdl_ctx* ctx, zdl_kernel_times* out);

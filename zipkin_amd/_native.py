@@ -33,6 +33,9 @@ EXPORTS = (
     "zdl_table_import", "zdl_get_kernel_times", "zdl_stream", "zdl_set_days", "zdl_link_days",
     "zdl_store_create", "zdl_store_destroy", "zdl_store_last_error", "zdl_store_append", "zdl_store_clear",
     "zdl_store_size", "zdl_put_stored",
+    "zdl_decoder_create", "zdl_decoder_destroy", "zdl_decoder_last_error", "zdl_decoder_bind",
+    "zdl_decoder_dict_size", "zdl_decoder_missing", "zdl_decode_proto3", "zdl_decode_proto3_retry",
+    "zdl_decoder_download",
 )
 
 
@@ -56,6 +59,11 @@ class DayLinks(C.Structure):
     _fields_ = [("n_days", C.c_uint64), ("day_ms", C.POINTER(C.c_int64)), ("n", C.c_uint64),
                 ("day", C.POINTER(C.c_int64)), ("parent", C.POINTER(C.c_int32)), ("child", C.POINTER(C.c_int32)),
                 ("call_count", C.POINTER(C.c_int64)), ("error_count", C.POINTER(C.c_int64))]
+
+
+class Decoded(C.Structure):
+    _fields_ = [("n_spans", C.c_uint64), ("dev", SpanCols), ("trace_lo", C.POINTER(C.c_uint64)),
+                ("timestamp", C.POINTER(C.c_int64)), ("n_missing", C.c_uint64)]
 
 
 class KernelTimes(C.Structure):
@@ -125,6 +133,22 @@ def lib() -> C.CDLL:
     L.zdl_put_stored.restype = C.c_int
     L.zdl_stream.restype = vp
     L.zdl_stream.argtypes = [vp]
+    L.zdl_decoder_create.restype = vp
+    L.zdl_decoder_create.argtypes = [C.c_int]
+    L.zdl_decoder_destroy.argtypes = [vp]
+    L.zdl_decoder_last_error.restype = C.c_char_p
+    L.zdl_decoder_last_error.argtypes = [vp]
+    L.zdl_decoder_bind.argtypes = [vp, C.c_int, C.c_char_p, u32, i32]
+    L.zdl_decoder_dict_size.restype = u64
+    L.zdl_decoder_dict_size.argtypes = [vp]
+    L.zdl_decoder_missing.argtypes = [vp, u64, C.POINTER(C.c_int), C.POINTER(C.POINTER(C.c_uint8)),
+                                      C.POINTER(u32)]
+    L.zdl_decode_proto3.argtypes = [vp, C.c_char_p, u64, C.POINTER(Decoded)]
+    L.zdl_decode_proto3_retry.argtypes = [vp, C.POINTER(Decoded)]
+    L.zdl_decoder_download.argtypes = [vp, C.POINTER(SpanCols)]
+    for name in ("zdl_decoder_bind", "zdl_decoder_missing", "zdl_decode_proto3", "zdl_decode_proto3_retry",
+                 "zdl_decoder_download"):
+        getattr(L, name).restype = C.c_int
     for name in ("zdl_set_ranks", "zdl_set_window", "zdl_put_spans", "zdl_put_spans_device", "zdl_sync",
                  "zdl_link", "zdl_merge_links", "zdl_add_links", "zdl_reset", "zdl_table_export",
                  "zdl_table_import", "zdl_get_kernel_times", "zdl_set_days", "zdl_link_days"):
@@ -286,6 +310,12 @@ class Store:
         self.h = C.c_void_p(h)
         self._L = L
 
+    def append_device(self, dev: SpanCols, n: int) -> None:
+        """Appends device columns (e.g. a Decoder's output) without a host round trip."""
+        rc = self._L.zdl_store_append(self.h, C.byref(dev), int(n))
+        if rc != ZDL_OK:
+            raise ZdlError(rc, self._L.zdl_store_last_error(self.h).decode())
+
     def append(self, cols) -> None:
         sc = SpanCols(None, _ptr(cols.id), _ptr(cols.parent_id), _ptr(cols.local_svc), _ptr(cols.remote_svc),
                       _ptr(cols.local_ip4), _ptr(cols.local_ip6), _ptr(cols.port_flags), _ptr(cols.timestamp))
@@ -302,6 +332,70 @@ class Store:
     def close(self):
         if getattr(self, "h", None):
             self._L.zdl_store_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Decoder:
+    """zdl_decoder: proto3 ListOfSpans -> device span columns (zdl_decode_proto3)."""
+
+    def __init__(self, device: int = 0):
+        L = lib()
+        h = L.zdl_decoder_create(int(device))
+        if not h:
+            raise ZdlError(ZDL_EDEVICE, "zdl_decoder_create failed")
+        self.h = C.c_void_p(h)
+        self._L = L
+
+    def check(self, rc: int):
+        if rc == ZDL_OK:
+            return
+        msg = self._L.zdl_decoder_last_error(self.h).decode()
+        if rc == ZDL_EREF_IAE:
+            raise ReferenceIllegalArgumentException(rc, msg)
+        raise ZdlError(rc, msg)
+
+    def decode(self, data: bytes) -> Decoded:
+        out = Decoded()
+        self.check(self._L.zdl_decode_proto3(self.h, bytes(data), len(data), C.byref(out)))
+        return out
+
+    def retry(self) -> Decoded:
+        out = Decoded()
+        self.check(self._L.zdl_decode_proto3_retry(self.h, C.byref(out)))
+        return out
+
+    def missing(self, n: int):
+        """[(dict, raw key bytes)] in first-seen (span, slot) order."""
+        res = []
+        for i in range(n):
+            k, p, ln = C.c_int(), C.POINTER(C.c_uint8)(), C.c_uint32()
+            self.check(self._L.zdl_decoder_missing(self.h, i, C.byref(k), C.byref(p), C.byref(ln)))
+            res.append((k.value, C.string_at(p, ln.value)))
+        return res
+
+    def bind(self, dict_id: int, key: bytes, id_: int):
+        self.check(self._L.zdl_decoder_bind(self.h, int(dict_id), bytes(key), len(key), int(id_)))
+
+    def download(self, n: int):
+        """The last decode's columns as host numpy arrays (dict by column name)."""
+        cols = dict(trace_lo=np.empty(n, np.uint64), id=np.empty(n, np.uint64), parent_id=np.empty(n, np.uint64),
+                    local_svc=np.empty(n, np.int32), remote_svc=np.empty(n, np.int32),
+                    local_ip4=np.empty(n, np.int32), local_ip6=np.empty(n, np.int32),
+                    port_flags=np.empty(n, np.uint32), timestamp=np.empty(n, np.int64))
+        sc = SpanCols(*(_ptr(cols[k]) for k in ("trace_lo", "id", "parent_id", "local_svc", "remote_svc",
+                                                 "local_ip4", "local_ip6", "port_flags", "timestamp")), None)
+        self.check(self._L.zdl_decoder_download(self.h, C.byref(sc)))
+        return cols
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._L.zdl_decoder_destroy(self.h)
             self.h = None
 
     def __del__(self):

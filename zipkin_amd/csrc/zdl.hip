@@ -1230,15 +1230,15 @@ int zdl_store_append(zdl_store* st, const zdl_span_cols* col, uint64_t n) {
     if (e == hipSuccess) st->cap = cap;
   }
   const uint64_t o = st->n;
-  if (e == hipSuccess) e = hipMemcpyAsync(st->id.p + o, col->id, n * 8, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess) e = hipMemcpyAsync(st->pid.p + o, col->parent_id, n * 8, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess) e = hipMemcpyAsync(st->lsvc.p + o, col->local_svc, n * 4, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess) e = hipMemcpyAsync(st->rsvc.p + o, col->remote_svc, n * 4, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess) e = hipMemcpyAsync(st->ip4.p + o, col->local_ip4, n * 4, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess) e = hipMemcpyAsync(st->ip6.p + o, col->local_ip6, n * 4, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess) e = hipMemcpyAsync(st->pf.p + o, col->port_flags, n * 4, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(st->id.p + o, col->id, n * 8, hipMemcpyDefault, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(st->pid.p + o, col->parent_id, n * 8, hipMemcpyDefault, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(st->lsvc.p + o, col->local_svc, n * 4, hipMemcpyDefault, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(st->rsvc.p + o, col->remote_svc, n * 4, hipMemcpyDefault, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(st->ip4.p + o, col->local_ip4, n * 4, hipMemcpyDefault, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(st->ip6.p + o, col->local_ip6, n * 4, hipMemcpyDefault, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(st->pf.p + o, col->port_flags, n * 4, hipMemcpyDefault, s);
   if (e == hipSuccess)
-    e = col->timestamp ? hipMemcpyAsync(st->ts.p + o, col->timestamp, n * 8, hipMemcpyHostToDevice, s)
+    e = col->timestamp ? hipMemcpyAsync(st->ts.p + o, col->timestamp, n * 8, hipMemcpyDefault, s)
                        : hipMemsetAsync(st->ts.p + o, 0, n * 8, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);  // the columns are borrowed for the call only
   if (e != hipSuccess)

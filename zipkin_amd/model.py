@@ -150,6 +150,39 @@ def _parse_ip(ip: str) -> Tuple[Optional[str], Optional[str]]:
     return None, addr.compressed
 
 
+def format_ipv6(ip: bytes) -> str:
+    """Endpoint.writeIpV6 (Endpoint.java:350-407): the text of 16 address bytes. The longest run
+    of zero groups ending before a non-zero group is compressed (first such run on ties); a
+    trailing run only when no earlier run ended."""
+    best_at, best_len, run_at, all_zero = -1, -1, -1, True
+    for i in range(0, 16, 2):
+        if ip[i] == 0 and ip[i + 1] == 0:
+            run_at = i if run_at < 0 else run_at
+            continue
+        all_zero = False
+        if run_at >= 0:
+            if i - run_at > best_len:
+                best_at, best_len = run_at, i - run_at
+            run_at = -1
+    if all_zero:
+        return "::"
+    if best_at == -1 and run_at != -1:
+        best_at, best_len = run_at, 16 - run_at
+    parts, i = [], 0
+    while i < 16:
+        if i == best_at:
+            parts.append(":")
+            i += best_len
+            if i == 16:
+                parts.append(":")
+            continue
+        if i != 0:
+            parts.append(":")
+        parts.append(format(ip[i] << 8 | ip[i + 1], "x"))  # hex without leading zeros
+        i += 2
+    return "".join(parts)
+
+
 def _norm_endpoint(e: Optional[Endpoint]) -> Optional[Endpoint]:
     if e is None or e.is_empty():
         return None

@@ -75,6 +75,7 @@ class InMemoryStorage:
         self._lo = np.zeros(0, np.uint64)
         self._ts = np.zeros(0, np.int64)
         self._alive = np.zeros(0, bool)
+        self._decoder = None  # proto3.Proto3Decoder, created on the first accept_proto3
 
     @staticmethod
     def new_builder():
@@ -103,6 +104,29 @@ class InMemoryStorage:
         # the reference accepts synchronously inside accept() (IMS:156-181)
         run()
         return Call(lambda: None)
+
+    def accept_proto3(self, data: bytes) -> Call[None]:
+        """``accept(SpanBytesDecoder.PROTO3.decodeList(data))`` with the decoding on the device
+        (zdl_decode_proto3): the decoded columns go from the decoder's HBM
+        buffers into the store without a host round trip; only the low trace ids and
+        timestamps come back for eviction and trace order. Raises
+        ReferenceIllegalArgumentException where the reference's decoder throws."""
+        if self._decoder is None:
+            from .proto3 import Proto3Decoder
+            self._decoder = Proto3Decoder(self._linker.svc, self._linker.ip4, self._linker.ip6, self.device)
+        b = self._decoder.decode(data)
+        if b.n_spans:
+            n_now = int(self._alive.sum())
+            self._evict((n_now + b.n_spans) - self.max_span_count)
+            if self._store is None:
+                self._store = N.Store(self.device)
+            self._store.append_device(b.dev, b.n_spans)
+            self._lo = np.concatenate([self._lo, b.trace_lo])
+            self._ts = np.concatenate([self._ts, b.timestamp])
+            self._alive = np.concatenate([self._alive, np.ones(b.n_spans, bool)])
+        return Call(lambda: None)
+
+    acceptProto3 = accept_proto3
 
     def _evict(self, to_recover: int):
         """deleteOldestTrace (IMS:193-211): the last key of TIMESTAMP_DESCENDING is the
