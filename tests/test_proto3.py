@@ -149,9 +149,9 @@ def add_unknown_fields(r, data: bytes) -> bytes:
         n = b.length_prefix()
         body = bytes(data[b.pos:b.pos + n])
         b.pos += n
-        extra = bytes([(20 << 3) | 0]) + P._varint(r.randrange(1 << 40))
-        extra += bytes([(21 << 3) | 1]) + struct.pack("<q", 7)
-        extra += bytes([(22 << 3) | 2, 3]) + b"xyz" + bytes([(23 << 3) | 5]) + b"abcd"
+        extra = P._varint(20 << 3 | 0) + P._varint(r.randrange(1 << 40))
+        extra += P._varint(21 << 3 | 1) + struct.pack("<q", 7)
+        extra += P._varint(22 << 3 | 2) + b"\x03xyz" + P._varint(23 << 3 | 5) + b"abcd"
         body = body + extra if r.random() < 0.5 else extra + body
         out += bytes([0x0a]) + P._varint(len(body)) + body
     return bytes(out)
