@@ -35,6 +35,53 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+# k_proto3_spans' compulsory traffic beyond the message bytes: span start (8) + length (4) read,
+# columns written (trace_lo, id, parent_id 8 each; 4 ids and port_flags 4 each; timestamp 8),
+# the per-span miss byte
+P3_BYTES_PER_SPAN = 12 + 52 + 1
+
+
+def proto3_leg(cols, w, S, device, doff, links, reps=5):
+    """Decode the batch's proto3 encoding on the device, then link the decoded columns with the
+    batch's trace offsets (the encoding keeps the span order): the links must equal the columnar
+    path's `links` by service name. Kernel time from HIP events around k_proto3_spans; the call
+    time includes the host's top-level scan, the PCIe upload and the trace-id/timestamp download."""
+    from zipkin_amd import synth
+    from zipkin_amd.columnar import Dictionary
+    from zipkin_amd import _native as N
+    from zipkin_amd.proto3 import Proto3Decoder
+    names = synth.service_names(w)
+    data = synth.encode_proto3(cols, names).tobytes()
+    dicts = (Dictionary(), Dictionary(), Dictionary())
+    dec = Proto3Decoder(*dicts, device=device)
+    b = dec.decode(data)  # first pass binds the names
+    ks, cs = [], []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        b = dec.decode(data)
+        cs.append(time.perf_counter() - t0)
+        ks.append(dec._dec.kernel_ms())
+    km, cm = float(np.median(ks)), float(np.median(cs)) * 1e3
+    svc = dicts[0]
+    ctx = N.Context(max(len(svc), 1), device=device)
+    dptr = {k: getattr(b.dev, k) for k in ("id", "parent_id", "local_svc", "remote_svc", "local_ip4",
+                                            "local_ip6", "port_flags")}
+    ctx.put_spans_device(dptr, b.n_spans, doff.data_ptr(), cols.n_traces)
+    gp, gc, gn, ge = ctx.link()
+    ctx.close()
+    got = sorted(zip((svc.strings[i] for i in gp.tolist()), (svc.strings[i] for i in gc.tolist()),
+                     gn.tolist(), ge.tolist()))
+    p, c, n, e = links
+    exp = sorted(zip((names[i] for i in p.tolist()), (names[i] for i in c.tolist()), n.tolist(), e.tolist()))
+    dec.close()
+    algo = len(data) + b.n_spans * P3_BYTES_PER_SPAN
+    return {"bytes": len(data), "spans": b.n_spans, "kernel_ms": km, "call_ms": cm,
+            "spans_per_s": b.n_spans / (km * 1e-3), "kernel_gbs": algo / (km * 1e-3) / 1e9,
+            "kernel_roofline_frac": algo / (km * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "algorithmic_bytes": algo, "call_spans_per_s": b.n_spans / (cm * 1e-3),
+            "parity": "same links" if got == exp else "MISMATCH"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -45,6 +92,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--cpu-sample-traces", type=int, default=200_000)
+    ap.add_argument("--no-proto3", action="store_true", help="skip the proto3 ingest side leg")
     ap.add_argument("--no-insertion-order", action="store_true",
                     help="skip the side measurement of the insertion-order mode (N = 1 only)")
     args = ap.parse_args()
@@ -153,6 +201,13 @@ def main():
         it = (time.perf_counter() - t1) / ik
         ictx.close()
         ins = {"ms_per_step": it * 1e3, "spans_per_s": cols.n_spans / it, "steps": ik, "parity": None}
+    # side measurement (not `value`): the same batch as a proto3 ListOfSpans decoded on the device
+    # (zdl_decode_proto3) and linked from the decoded HBM columns
+    p3 = None
+    if world == 1 and not args.no_proto3:
+        p3 = proto3_leg(cols, w, S, local, doff, (p, c, n, e))
+        log(f"proto3 ingest: kernel {p3['kernel_ms']:.3f} ms ({p3['kernel_gbs']:.0f} GB/s), "
+            f"call {p3['call_ms']:.1f} ms, links {p3['parity']}")
     parity = None
     cpu = None
     if rank == 0 and world == 1 and not args.no_parity:
@@ -221,7 +276,8 @@ def main():
                        "services": S, "parallelism": f"trace-shard x{world}" + (" + RCCL all-reduce" if world > 1 else ""),
                        "kernel_ms": {"k_link": tiles},
                        "step_roofline_frac": bytes_path / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                       "parity": parity, "links": int(len(p)), "insertion_order": ins},
+                       "parity": parity, "links": int(len(p)), "insertion_order": ins,
+                       "proto3_ingest": p3},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "k_link", "algorithmic_bytes_per_launch": bytes_launch},

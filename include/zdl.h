@@ -267,6 +267,7 @@ void         zdl_decoder_destroy(zdl_decoder* dec);
 const char*  zdl_decoder_last_error(const zdl_decoder* dec);
 int          zdl_decoder_bind(zdl_decoder* dec, int dict, const uint8_t* key, uint32_t len, int32_t id);
 uint64_t     zdl_decoder_dict_size(const zdl_decoder* dec);
+float        zdl_decoder_kernel_ms(const zdl_decoder* dec);  /* HIP-event time of the last decode kernel */
 int          zdl_decoder_missing(const zdl_decoder* dec, uint64_t i, int* dict, const uint8_t** key,
                                  uint32_t* len);
 int          zdl_decode_proto3(zdl_decoder* dec, const uint8_t* bytes, uint64_t len, zdl_decoded* out);

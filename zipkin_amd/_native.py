@@ -35,7 +35,7 @@ EXPORTS = (
     "zdl_store_size", "zdl_put_stored",
     "zdl_decoder_create", "zdl_decoder_destroy", "zdl_decoder_last_error", "zdl_decoder_bind",
     "zdl_decoder_dict_size", "zdl_decoder_missing", "zdl_decode_proto3", "zdl_decode_proto3_retry",
-    "zdl_decoder_download",
+    "zdl_decoder_download", "zdl_decoder_kernel_ms",
 )
 
 
@@ -146,6 +146,8 @@ def lib() -> C.CDLL:
     L.zdl_decode_proto3.argtypes = [vp, C.c_char_p, u64, C.POINTER(Decoded)]
     L.zdl_decode_proto3_retry.argtypes = [vp, C.POINTER(Decoded)]
     L.zdl_decoder_download.argtypes = [vp, C.POINTER(SpanCols)]
+    L.zdl_decoder_kernel_ms.restype = C.c_float
+    L.zdl_decoder_kernel_ms.argtypes = [vp]
     for name in ("zdl_decoder_bind", "zdl_decoder_missing", "zdl_decode_proto3", "zdl_decode_proto3_retry",
                  "zdl_decoder_download"):
         getattr(L, name).restype = C.c_int
@@ -392,6 +394,9 @@ class Decoder:
                                                  "local_ip4", "local_ip6", "port_flags", "timestamp")), None)
         self.check(self._L.zdl_decoder_download(self.h, C.byref(sc)))
         return cols
+
+    def kernel_ms(self) -> float:
+        return float(self._L.zdl_decoder_kernel_ms(self.h))
 
     def close(self):
         if getattr(self, "h", None):

@@ -354,3 +354,86 @@ void zdl_synth_fill(const zdl_synth_params* p, const uint64_t* offsets, uint64_t
 }
 
 }  // extern "C"
+
+// ---- proto3 encoding of synthetic columns (bench / test input for zdl_decode_proto3) ----
+// Writes a ListOfSpans (Proto3ZipkinFields.java:246-302 field order) for spans [0, n) of the
+// columns: trace_id (8 bytes), parent_id, id, kind, timestamp, local endpoint {service name,
+// ipv4 10.a.b.c from the ipv4 id, port}, remote endpoint {service name, port 80 when RPORT},
+// tag error="" when the error flag is set, shared when shared == true. Service id i is
+// names[name_off[i], name_off[i+1]). Returns the byte count; out == NULL only measures.
+namespace {
+inline size_t put_varint(uint8_t* o, uint64_t v) {
+  size_t k = 0;
+  while (v >= 0x80) {
+    if (o) o[k] = (uint8_t)(v | 0x80);
+    v >>= 7;
+    ++k;
+  }
+  if (o) o[k] = (uint8_t)v;
+  return k + 1;
+}
+inline size_t varint_len(uint64_t v) { return put_varint(nullptr, v); }
+inline void put_be64(uint8_t* o, uint64_t v) {
+  for (int i = 7; i >= 0; --i) o[7 - i] = (uint8_t)(v >> (8 * i));
+}
+}  // namespace
+
+extern "C" uint64_t zdl_synth_proto3(uint64_t n, const uint64_t* trace_lo, const uint64_t* id,
+                                     const uint64_t* parent_id, const int32_t* local_svc,
+                                     const int32_t* remote_svc, const int32_t* local_ip4,
+                                     const uint32_t* port_flags, const int64_t* timestamp,
+                                     const char* names, const uint32_t* name_off, uint8_t* out) {
+  uint64_t pos = 0;
+  uint8_t span[512];
+  for (uint64_t i = 0; i < n; ++i) {
+    size_t k = 0;
+    span[k++] = 1 << 3 | 2, span[k++] = 8, put_be64(span + k, trace_lo[i]), k += 8;
+    if (parent_id[i]) span[k++] = 2 << 3 | 2, span[k++] = 8, put_be64(span + k, parent_id[i]), k += 8;
+    span[k++] = 3 << 3 | 2, span[k++] = 8, put_be64(span + k, id[i]), k += 8;
+    const uint32_t pf = port_flags[i];
+    const uint32_t kind = (pf >> 16) & 7;
+    if (kind != 7) span[k++] = 4 << 3, span[k++] = (uint8_t)(kind + 1);
+    if (timestamp[i] > 0) {
+      span[k++] = 6 << 3 | 1;
+      for (int b = 0; b < 8; ++b) span[k++] = (uint8_t)((uint64_t)timestamp[i] >> (8 * b));
+    }
+    for (int side = 0; side < 2; ++side) {
+      const int32_t svc = side ? remote_svc[i] : local_svc[i];
+      const int32_t ip = side ? -1 : local_ip4[i];
+      const uint32_t port = side ? ((pf >> 24 & 1) ? 80u : 0u) : (pf & 0xFFFF);
+      uint8_t ep[256];
+      size_t e = 0;
+      if (svc >= 0) {
+        const uint32_t l = name_off[svc + 1] - name_off[svc];
+        ep[e++] = 1 << 3 | 2;
+        e += put_varint(ep + e, l);
+        memcpy(ep + e, names + name_off[svc], l);
+        e += l;
+      }
+      if (ip >= 0) {
+        ep[e++] = 2 << 3 | 2, ep[e++] = 4, ep[e++] = 10;
+        ep[e++] = (uint8_t)(ip >> 16), ep[e++] = (uint8_t)(ip >> 8), ep[e++] = (uint8_t)ip;
+      }
+      if (port) ep[e++] = 4 << 3, e += put_varint(ep + e, port);
+      if (!e) continue;
+      span[k++] = (uint8_t)((8 + side) << 3 | 2);
+      k += put_varint(span + k, e);
+      memcpy(span + k, ep, e);
+      k += e;
+    }
+    if (pf & (1u << 21)) {  // tags {"error": ""}: the map entry carries only its key
+      const uint8_t tag[] = {11 << 3 | 2, 7, 1 << 3 | 2, 5, 'e', 'r', 'r', 'o', 'r'};
+      memcpy(span + k, tag, sizeof(tag));
+      k += sizeof(tag);
+    }
+    if (((pf >> 19) & 3) == 2) span[k++] = 13 << 3, span[k++] = 1;
+    const size_t hdr = 1 + varint_len(k);
+    if (out) {
+      out[pos] = 1 << 3 | 2;
+      put_varint(out + pos + 1, k);
+      memcpy(out + pos + hdr, span, k);
+    }
+    pos += hdr + k;
+  }
+  return pos;
+}

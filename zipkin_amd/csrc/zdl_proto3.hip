@@ -522,6 +522,8 @@ struct zdl_decoder {
   HBuf<uint64_t> lo_h;
   HBuf<int64_t> ts_h;
   std::vector<std::string> missing;  // kind byte + key bytes, first-seen order
+  hipEvent_t ev[2] = {nullptr, nullptr};  // around the last k_proto3_spans
+  float kernel_ms = 0.f;
 };
 
 namespace {
@@ -579,11 +581,14 @@ int run_kernel(zdl_decoder* d, zdl_decoded* out) {
     Dict dict{d->slots.p, d->arena.p, d->cap ? d->cap - 1 : 0};
     Out o{d->lo.p,   d->id.p, d->pid.p, d->lsvc.p,     d->rsvc.p,     d->ip4.p,    d->ip6.p,
           d->pf.p,   d->ts.p, d->miss.p, d->miss_off.p, d->miss_len.p, d->status.p, (uint32_t*)(d->status.p + 1)};
+    DEC_TRY(d, hipEventRecord(d->ev[0], s));
     k_proto3_spans<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(d->buf.p, d->len, d->start.p, d->slen.p, (uint32_t)n,
                                                                 dict, o);
     DEC_TRY(d, hipGetLastError());
+    DEC_TRY(d, hipEventRecord(d->ev[1], s));
     DEC_TRY(d, hipMemcpyAsync(d->status_h.p, d->status.p, 16, hipMemcpyDeviceToHost, s));
     DEC_TRY(d, hipStreamSynchronize(s));
+    DEC_TRY(d, hipEventElapsedTime(&d->kernel_ms, d->ev[0], d->ev[1]));
     const unsigned long long fe = d->status_h.p[0];
     if (fe != kNoErr)  // the first failing span decides, before the scan's own verdict
       return (fe & 1) ? dfail(d, ZDL_EREF_IAE, "reference throws IllegalArgumentException reading List<Span> from proto3 (span " +
@@ -644,7 +649,8 @@ zdl_decoder* zdl_decoder_create(int device) {
   if (!d) return nullptr;
   d->device = device;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess ||
-      d->status.ensure(2) != hipSuccess || d->status_h.ensure(2) != hipSuccess) {
+      d->status.ensure(2) != hipSuccess || d->status_h.ensure(2) != hipSuccess ||
+      hipEventCreate(&d->ev[0]) != hipSuccess || hipEventCreate(&d->ev[1]) != hipSuccess) {
     if (d->stream) (void)hipStreamDestroy(d->stream);
     delete d;
     return nullptr;
@@ -657,6 +663,8 @@ void zdl_decoder_destroy(zdl_decoder* d) {
   (void)hipSetDevice(d->device);
   if (d->stream) (void)hipStreamSynchronize(d->stream);
   hipStream_t s = d->stream;
+  for (hipEvent_t e : d->ev)
+    if (e) (void)hipEventDestroy(e);
   delete d;  // buffers free themselves
   if (s) (void)hipStreamDestroy(s);
 }
@@ -676,6 +684,8 @@ int zdl_decoder_bind(zdl_decoder* d, int kind, const uint8_t* key, uint32_t len,
 }
 
 uint64_t zdl_decoder_dict_size(const zdl_decoder* d) { return d ? d->keys.size() : 0; }
+
+float zdl_decoder_kernel_ms(const zdl_decoder* d) { return d ? d->kernel_ms : 0.f; }
 
 int zdl_decoder_missing(const zdl_decoder* d, uint64_t i, int* kind, const uint8_t** key, uint32_t* len) {
   if (!d || i >= d->missing.size() || !kind || !key || !len) return ZDL_EINVAL;

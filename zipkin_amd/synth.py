@@ -126,3 +126,23 @@ def generate(w: Workload, threads: int = 0) -> Columns:
 
 def service_names(w: Workload):
     return [f"svc-{i:05d}" for i in range(w.n_services)] + [f"zkafka-{i}" for i in range(w.n_brokers)]
+
+
+def encode_proto3(cols: Columns, names) -> np.ndarray:
+    """The spans of `cols` (in column order) as one proto3 ListOfSpans (zdl_synth_proto3 in
+    csrc/synth.cpp): what a collector would receive for the same batch. `names[i]` is service i."""
+    L = _synth()
+    if not hasattr(L, "_p3"):
+        L.zdl_synth_proto3.restype = C.c_uint64
+        L.zdl_synth_proto3.argtypes = [C.c_uint64] + [C.c_void_p] * 11
+        L._p3 = True
+    blob = "".join(names).encode()
+    off = np.zeros(len(names) + 1, np.uint32)
+    off[1:] = np.cumsum([len(x.encode()) for x in names])
+    args = [cols.trace_lo, cols.id, cols.parent_id, cols.local_svc, cols.remote_svc, cols.local_ip4,
+            cols.port_flags, cols.timestamp]
+    ptrs = [a.ctypes.data for a in args] + [C.c_char_p(blob), off.ctypes.data]
+    n = L.zdl_synth_proto3(cols.n_spans, *ptrs, None)
+    out = np.empty(n, np.uint8)
+    L.zdl_synth_proto3(cols.n_spans, *ptrs, out.ctypes.data)
+    return out
