@@ -325,3 +325,20 @@ def test_gpu_decode_then_link_large():
     exp = sorted(zip(*(a.tolist() for a in ctx2.link())))
     assert got == exp and len(got) > 0
     dec.close()
+
+
+@pytest.mark.gpu
+def test_gpu_decode_spans_beyond_lds_window():
+    """Blocks whose span messages exceed the kernel's LDS window read the rest from HBM."""
+    from zipkin_amd.proto3 import Proto3Decoder
+    r = random.Random(3)
+    sp = rand_batch(r, 600)
+    big = [s.to_builder(local_endpoint=Endpoint.create("svc-" + "x" * r.randrange(50, 3000), "10.0.0.1", 80))
+           if i % 3 == 0 else s for i, s in enumerate(sp)]
+    d, o = fresh(), fresh()
+    dec = Proto3Decoder(*d)
+    data = P.write_list(big)
+    exp, _ = oracle_columns(data, *o)
+    assert_same(dec.decode_columns(data), exp)
+    assert [x.strings for x in d] == [x.strings for x in o]
+    dec.close()

@@ -53,15 +53,19 @@ struct Dict {
   uint32_t mask;  // capacity - 1
 };
 
-__host__ __device__ inline uint64_t key_hash(int kind, const uint8_t* p, uint32_t n) {
+template <class Get>
+__host__ __device__ inline uint64_t key_hash(int kind, Get get, uint32_t n) {
   uint64_t h = 1469598103934665603ull ^ (uint64_t)(kind + 1);
   h *= 1099511628211ull;
   for (uint32_t i = 0; i < n; ++i) {
-    h ^= p[i];
+    h ^= get(i);
     h *= 1099511628211ull;
   }
   return h ^ (h >> 29);
 }
+
+constexpr int kBlock = 256;
+constexpr uint32_t kWin = 24 * 1024;  // LDS window per block: the block's span messages (C2: ~19 KB)
 
 struct Out {
   uint64_t *trace_lo, *id, *pid;
@@ -78,20 +82,27 @@ struct Out {
 enum : int { SLOT_LSVC = 0, SLOT_LIP4 = 1, SLOT_LIP6 = 2, SLOT_RSVC = 3 };
 enum : int { F_OK = 0, F_IAE = 1, F_OVERRUN = 2 };
 
-// Buffer over the whole batch (bounds = the batch, as in Buffer.java); fail is sticky.
+// Buffer over the whole batch (bounds = the batch, as in Buffer.java); fail is sticky. Bytes
+// inside the block's LDS window [w0, w0 + wn) are read from LDS, the rest from HBM.
 struct Rd {
   const uint8_t* b;
   uint64_t n, pos;
   int fail;
+  const uint8_t* w;
+  uint64_t w0, wn;
 
-  __device__ uint8_t byte() {
+  __device__ __forceinline__ uint8_t at(uint64_t p) const {
+    const uint64_t q = p - w0;
+    return q < wn ? w[q] : b[p];
+  }
+  __device__ __forceinline__ uint8_t byte() {
     if (pos >= n) {
       fail = fail ? fail : F_IAE;  // "Truncated reading position"
       return 0;
     }
-    return b[pos++];
+    return at(pos++);
   }
-  __device__ int32_t varint32() {  // Buffer.readVarint32
+  __device__ __forceinline__ int32_t varint32() {  // Buffer.readVarint32
     uint32_t r = 0;
     for (int i = 0; i < 4; ++i) {
       const uint8_t x = byte();
@@ -103,45 +114,45 @@ struct Rd {
       fail = F_IAE;
       return 0;
     }
-    const uint8_t x = b[pos];  // not advanced (Buffer.java:328-333)
+    const uint8_t x = at(pos);  // not advanced (Buffer.java:328-333)
     if (x & 0xF0) {
       fail = F_IAE;
       return 0;
     }
     return (int32_t)(r | (uint32_t)x << 28);
   }
-  __device__ void varint64() {  // Buffer.readVarint64, value unused
+  __device__ __forceinline__ void varint64() {  // Buffer.readVarint64, value unused
     uint8_t x = byte();
     for (int i = 1; !fail && x >= 0x80 && i < 10; ++i) {
       x = byte();
       if (!fail && i == 9 && (x & 0xF0)) fail = F_IAE;
     }
   }
-  __device__ int64_t remaining() const { return (int64_t)(n - pos); }
-  __device__ int32_t length_prefix() {  // readLengthPrefix + ensureLength
+  __device__ __forceinline__ int64_t remaining() const { return (int64_t)(n - pos); }
+  __device__ __forceinline__ int32_t length_prefix() {  // readLengthPrefix + ensureLength
     const int32_t len = varint32();
     if (!fail && (int64_t)len > remaining()) fail = F_IAE;
     return len;
   }
-  __device__ int64_t fixed64() {  // Fixed64Field.readValue
+  __device__ __forceinline__ int64_t fixed64() {  // Fixed64Field.readValue
     if (remaining() < 8) {
       fail = F_IAE;
       return 0;
     }
     uint64_t v = 0;
-    for (int i = 0; i < 8; ++i) v |= (uint64_t)b[pos + i] << (8 * i);
+    for (int i = 0; i < 8; ++i) v |= (uint64_t)at(pos + i) << (8 * i);
     pos += 8;
     return (int64_t)v;
   }
-  __device__ void clamp_skip(int64_t k) {  // Buffer.skip
+  __device__ __forceinline__ void clamp_skip(int64_t k) {  // Buffer.skip
     pos = (pos + (uint64_t)k > n) ? n : pos + (uint64_t)k;
   }
-  __device__ void skip_value(int32_t key) {  // logAndSkip -> skipValue
+  __device__ __forceinline__ void skip_value(int32_t key) {  // logAndSkip -> skipValue
     switch (key & 7) {
       case 0: {
         const int64_t rem = remaining();
         for (int64_t i = 0; i < rem; ++i)
-          if (b[pos++] < 0x80) return;
+          if (at(pos++) < 0x80) return;
         return;
       }
       case 1: clamp_skip(8); return;
@@ -157,11 +168,11 @@ struct Rd {
     }
   }
   // a nested loop over [pos, end) finished: reading past `end` is the lenient case
-  __device__ void close(int64_t end) {
+  __device__ __forceinline__ void close(int64_t end) {
     if (!fail && (int64_t)pos > end) fail = F_OVERRUN;
   }
   // a string / bytes field of length len (0 = null): positive lengths are skipped
-  __device__ bool take(int32_t len, uint64_t* off) {
+  __device__ __forceinline__ bool take(int32_t len, uint64_t* off) {
     if (fail) return false;
     if (len < 0) {  // new byte[negative] / new String(.., negative)
       fail = F_IAE;
@@ -180,20 +191,20 @@ struct Ep {  // Endpoint.Builder state for the columns
   bool has4 = false, has6 = false;
   uint64_t ip6_off = 0;
   int32_t port = 0;
-  __device__ bool empty() const { return !svc_len && !has4 && !has6 && !port; }
+  __device__ __forceinline__ bool empty() const { return !svc_len && !has4 && !has6 && !port; }
 };
 
-__device__ void parse_ip(Rd& r, uint64_t off, int32_t len, Ep& e) {  // Endpoint.Builder.parseIp(byte[])
-  const uint8_t* p = r.b + off;
+__device__ __forceinline__ void parse_ip(Rd& r, uint64_t off, int32_t len, Ep& e) {  // Endpoint.Builder.parseIp(byte[])
+  auto p = [&](int i) { return (uint32_t)r.at(off + i); };
   if (len == 4) {
-    e.ip4 = (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3];
+    e.ip4 = p(0) << 24 | p(1) << 16 | p(2) << 8 | p(3);
     e.has4 = true;
   } else if (len == 16) {
     bool z = true;
-    for (int i = 0; i < 12; ++i) z &= p[i] == 0;  // 80 zero bits and flag == 0 (flag == -1 never holds)
-    const bool loop = z && p[12] == 0 && p[13] == 0 && p[14] == 0 && p[15] == 1;  // ::1
+    for (int i = 0; i < 12; ++i) z &= p(i) == 0;  // 80 zero bits and flag == 0 (flag == -1 never holds)
+    const bool loop = z && p(12) == 0 && p(13) == 0 && p(14) == 0 && p(15) == 1;  // ::1
     if (z && !loop) {
-      e.ip4 = (uint32_t)p[12] << 24 | (uint32_t)p[13] << 16 | (uint32_t)p[14] << 8 | p[15];
+      e.ip4 = p(12) << 24 | p(13) << 16 | p(14) << 8 | p(15);
       e.has4 = true;
     } else {
       e.ip6_off = off;
@@ -202,7 +213,7 @@ __device__ void parse_ip(Rd& r, uint64_t off, int32_t len, Ep& e) {  // Endpoint
   }
 }
 
-__device__ void read_endpoint(Rd& r, int32_t len, Ep& e) {  // EndpointField.readValue
+__device__ __forceinline__ void read_endpoint(Rd& r, int32_t len, Ep& e) {  // EndpointField.readValue
   e = Ep();
   const int64_t end = (int64_t)r.pos + len;  // before pos when len < 0: nothing read, then close()
   while (!r.fail && (int64_t)r.pos < end) {
@@ -227,18 +238,19 @@ __device__ void read_endpoint(Rd& r, int32_t len, Ep& e) {  // EndpointField.rea
   r.close(end);
 }
 
-__device__ bool bytes_are_error(const uint8_t* p) {
-  return p[0] == 'e' && p[1] == 'r' && p[2] == 'r' && p[3] == 'o' && p[4] == 'r';
+__device__ __forceinline__ bool bytes_are_error(const Rd& r, uint64_t o) {
+  return r.at(o) == 'e' && r.at(o + 1) == 'r' && r.at(o + 2) == 'r' && r.at(o + 3) == 'o' && r.at(o + 4) == 'r';
 }
 
 // hex id of L bytes -> value; rules of Span.Builder.traceId / id / parentId
-__device__ uint64_t be_tail(const uint8_t* p, int32_t n) {
+__device__ __forceinline__ uint64_t be_tail(const Rd& r, uint64_t off, int32_t n) {
   uint64_t v = 0;
-  for (int32_t i = n > 8 ? n - 8 : 0; i < n; ++i) v = v << 8 | p[i];
+  for (int32_t i = n > 8 ? n - 8 : 0; i < n; ++i) v = v << 8 | r.at(off + i);
   return v;
 }
 
-__device__ int32_t lookup(const Dict& d, int kind, const uint8_t* p, uint32_t n) {
+template <class Get>
+__device__ __forceinline__ int32_t lookup(const Dict& d, int kind, Get p, uint32_t n) {
   if (d.mask == 0) return -2;
   const uint64_t h = key_hash(kind, p, n);
   for (uint32_t i = (uint32_t)h & d.mask, probes = 0; probes <= d.mask; i = (i + 1) & d.mask, ++probes) {
@@ -249,19 +261,34 @@ __device__ int32_t lookup(const Dict& d, int kind, const uint8_t* p, uint32_t n)
     const uint32_t kl = (uint32_t)k[0] | (uint32_t)k[1] << 8 | (uint32_t)k[2] << 16 | (uint32_t)k[3] << 24;
     if (kl != n || k[4] != (uint8_t)kind) continue;
     bool eq = true;
-    for (uint32_t j = 0; j < n && eq; ++j) eq = k[5 + j] == p[j];
+    for (uint32_t j = 0; j < n && eq; ++j) eq = k[5 + j] == p(j);
     if (eq) return s.id;
   }
   return -2;
 }
 
-__global__ void __launch_bounds__(256) k_proto3_spans(const uint8_t* __restrict__ buf, uint64_t len,
-                                                        const uint64_t* __restrict__ start,
-                                                        const uint32_t* __restrict__ slen, uint32_t n, Dict dict,
-                                                        Out o) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ void __launch_bounds__(kBlock) k_proto3_spans(const uint8_t* __restrict__ buf, uint64_t len,
+                                                           const uint64_t* __restrict__ start,
+                                                           const uint32_t* __restrict__ slen, uint32_t n, Dict dict,
+                                                           Out o) {
+  // The block's span messages are contiguous in the batch: stage them in LDS with coalesced
+  // 16-byte loads (from a 16-byte aligned base), so the byte-serial parsing below reads LDS.
+  __shared__ __attribute__((aligned(16))) uint8_t win[kWin];
+  const uint32_t first = blockIdx.x * kBlock;
+  const uint32_t last = min(first + kBlock, n) - 1;
+  const uint64_t w0 = start[first] & ~15ull;
+  const uint64_t wn = min<uint64_t>(start[last] + slen[last] - w0, kWin);
+  for (uint64_t q = (uint64_t)threadIdx.x * 16; q < wn; q += kBlock * 16) {
+    if (w0 + q + 16 <= len) {
+      *(uint4*)(win + q) = *(const uint4*)(buf + w0 + q);
+    } else {
+      for (uint64_t t = q; t < q + 16 && w0 + t < len; ++t) win[t] = buf[w0 + t];
+    }
+  }
+  __syncthreads();
+  const uint32_t i = first + threadIdx.x;
   if (i >= n) return;
-  Rd r{buf, len, start[i], F_OK};
+  Rd r{buf, len, start[i], F_OK, win, w0, wn};
   const int64_t end = (int64_t)(r.pos + slen[i]);
   bool has_trace = false, has_id = false, shared = false, error = false;
   uint64_t lo = 0, id = 0, pid = 0;
@@ -278,9 +305,9 @@ __global__ void __launch_bounds__(256) k_proto3_spans(const uint8_t* __restrict_
         if (!r.take(m, &off) && !r.fail) r.fail = F_IAE;  // traceId == null
         if (r.fail) break;
         bool zero = true;
-        for (int32_t j = 0; j < m; ++j) zero &= buf[off + j] == 0;
+        for (int32_t j = 0; j < m; ++j) zero &= r.at(off + j) == 0;
         if (m > 16 || zero) r.fail = F_IAE;  // length > 32 hex / all zeros
-        lo = be_tail(buf + off, m);
+        lo = be_tail(r, off, m);
         has_trace = true;
         break;
       }
@@ -291,7 +318,7 @@ __global__ void __launch_bounds__(256) k_proto3_spans(const uint8_t* __restrict_
           break;
         }
         if (m > 8) r.fail = F_IAE;
-        pid = be_tail(buf + off, m);  // all zeros -> null (0)
+        pid = be_tail(r, off, m);  // all zeros -> null (0)
         break;
       }
       case 3 << 3 | 2: {  // id
@@ -299,7 +326,7 @@ __global__ void __launch_bounds__(256) k_proto3_spans(const uint8_t* __restrict_
         if (!r.take(m, &off) && !r.fail) r.fail = F_IAE;  // id == null
         if (r.fail) break;
         if (m > 8) r.fail = F_IAE;
-        id = be_tail(buf + off, m);
+        id = be_tail(r, off, m);
         if (m == 8 && id == 0) r.fail = F_IAE;  // "id is all zeros" (16 zero hex digits only)
         has_id = true;
         break;
@@ -320,11 +347,12 @@ __global__ void __launch_bounds__(256) k_proto3_spans(const uint8_t* __restrict_
       case 7 << 3 | 0: r.varint64(); break;  // duration
       case 8 << 3 | 2:
       case 9 << 3 | 2: {
-        Ep& e = key == (8 << 3 | 2) ? le : re;
         const int32_t m = r.length_prefix();
         if (r.fail) break;
-        if (m == 0) e = Ep();  // readLengthPrefixAndValue -> null endpoint
-        else read_endpoint(r, m, e);
+        Ep e;  // m == 0: readLengthPrefixAndValue -> null endpoint
+        if (m != 0) read_endpoint(r, m, e);
+        if (key == (8 << 3 | 2)) le = e;  // no reference select: both stay in registers
+        else re = e;
         break;
       }
       case 10 << 3 | 2: {  // annotation: validated, not kept
@@ -360,7 +388,7 @@ __global__ void __launch_bounds__(256) k_proto3_spans(const uint8_t* __restrict_
           }
         }
         r.close(te);
-        if (!r.fail && klen == 5 && bytes_are_error(buf + koff)) error = true;
+        if (!r.fail && klen == 5 && bytes_are_error(r, koff)) error = true;
         break;
       }
       case 12 << 3 | 0:
@@ -387,20 +415,20 @@ __global__ void __launch_bounds__(256) k_proto3_spans(const uint8_t* __restrict_
   uint64_t moff[4] = {0, 0, 0, 0};
   uint32_t mlen[4] = {0, 0, 0, 0};
   if (!lnull && le.svc_len) {
-    ls = lookup(dict, ZDL_DICT_SERVICE, buf + le.svc_off, le.svc_len);
+    ls = lookup(dict, ZDL_DICT_SERVICE, [&](uint32_t j) { return r.at(le.svc_off + j); }, le.svc_len);
     moff[SLOT_LSVC] = le.svc_off, mlen[SLOT_LSVC] = le.svc_len;
   }
   if (!lnull && le.has4) {
     const uint8_t k[4] = {(uint8_t)(le.ip4 >> 24), (uint8_t)(le.ip4 >> 16), (uint8_t)(le.ip4 >> 8), (uint8_t)le.ip4};
-    l4 = lookup(dict, ZDL_DICT_IPV4, k, 4);
+    l4 = lookup(dict, ZDL_DICT_IPV4, [&](uint32_t j) { return k[j]; }, 4);
     moff[SLOT_LIP4] = le.ip4, mlen[SLOT_LIP4] = 4;
   }
   if (!lnull && le.has6) {
-    l6 = lookup(dict, ZDL_DICT_IPV6, buf + le.ip6_off, 16);
+    l6 = lookup(dict, ZDL_DICT_IPV6, [&](uint32_t j) { return r.at(le.ip6_off + j); }, 16);
     moff[SLOT_LIP6] = le.ip6_off, mlen[SLOT_LIP6] = 16;
   }
   if (!rnull && re.svc_len) {
-    rs = lookup(dict, ZDL_DICT_SERVICE, buf + re.svc_off, re.svc_len);
+    rs = lookup(dict, ZDL_DICT_SERVICE, [&](uint32_t j) { return r.at(re.svc_off + j); }, re.svc_len);
     moff[SLOT_RSVC] = re.svc_off, mlen[SLOT_RSVC] = re.svc_len;
   }
   miss = (ls == -2) | (l4 == -2) << 1 | (l6 == -2) << 2 | (rs == -2) << 3;
@@ -500,11 +528,10 @@ struct zdl_decoder {
   DBuf<uint8_t> arena;
   uint32_t cap = 0;
   // the resident batch
-  std::vector<uint8_t> host_copy;  // raw bytes, for reporting missing keys
   DBuf<uint8_t> buf;
   DBuf<uint64_t> start;
   DBuf<uint32_t> slen;
-  HBuf<uint8_t> stage;
+  HBuf<uint8_t> stage;  // pinned copy of the batch: the upload source, and where missing keys are read
   std::vector<uint64_t> start_h;
   std::vector<uint32_t> slen_h;
   uint64_t len = 0, n = 0;
@@ -553,7 +580,8 @@ int upload_dict(zdl_decoder* d) {
     const uint32_t kl = (uint32_t)(k.size() - 1);
     for (int b = 0; b < 4; ++b) d->arena_h.push_back((uint8_t)(kl >> (8 * b)));
     d->arena_h.insert(d->arena_h.end(), k.begin(), k.end());
-    const uint64_t h = key_hash((uint8_t)k[0], (const uint8_t*)k.data() + 1, kl);
+    const uint8_t* kb = (const uint8_t*)k.data() + 1;
+    const uint64_t h = key_hash((uint8_t)k[0], [kb](uint32_t j) { return kb[j]; }, kl);
     uint32_t i = (uint32_t)h & (cap - 1);
     while (sl[i].koff != kNoKey) i = (i + 1) & (cap - 1);
     sl[i] = Slot{h, koff, kv.second};
@@ -582,7 +610,7 @@ int run_kernel(zdl_decoder* d, zdl_decoded* out) {
     Out o{d->lo.p,   d->id.p, d->pid.p, d->lsvc.p,     d->rsvc.p,     d->ip4.p,    d->ip6.p,
           d->pf.p,   d->ts.p, d->miss.p, d->miss_off.p, d->miss_len.p, d->status.p, (uint32_t*)(d->status.p + 1)};
     DEC_TRY(d, hipEventRecord(d->ev[0], s));
-    k_proto3_spans<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(d->buf.p, d->len, d->start.p, d->slen.p, (uint32_t)n,
+    k_proto3_spans<<<(unsigned)((n + kBlock - 1) / kBlock), kBlock, 0, s>>>(d->buf.p, d->len, d->start.p, d->slen.p, (uint32_t)n,
                                                                 dict, o);
     DEC_TRY(d, hipGetLastError());
     DEC_TRY(d, hipEventRecord(d->ev[1], s));
@@ -618,7 +646,7 @@ int run_kernel(zdl_decoder* d, zdl_decoded* out) {
         if (sl == SLOT_LIP4) {
           for (int b = 3; b >= 0; --b) k.push_back((char)(uint8_t)(off >> (8 * b)));
         } else {
-          k.append((const char*)d->host_copy.data() + off, ml[4 * i + sl]);
+          k.append((const char*)d->stage.p + off, ml[4 * i + sl]);
         }
         if (seen.emplace(k, true).second) d->missing.push_back(k);
       }
@@ -729,7 +757,6 @@ int zdl_decode_proto3(zdl_decoder* d, const uint8_t* data, uint64_t len, zdl_dec
   const uint64_t n = d->start_h.size();
   d->n = n;
   d->len = len;
-  d->host_copy.assign(data, data + len);
   const hipStream_t s = d->stream;
   if (n) {
     DEC_TRY(d, d->stage.ensure(len));
