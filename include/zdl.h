@@ -275,6 +275,35 @@ int          zdl_decode_proto3_retry(zdl_decoder* dec, zdl_decoded* out);
 /* copies the last decode's device columns into the non-NULL host columns of dst */
 int          zdl_decoder_download(zdl_decoder* dec, const zdl_span_cols* dst);
 
+/* ---- mysql-v1 rows: AggregateDependencies.apply's loop
+ * (zipkin-storage/mysql-v1/.../AggregateDependencies.java:71-84) over its cursor: rows grouped by
+ * trace then span id (the query's groupBy), each span's rows projected to a minimal span by
+ * DependencyLinkV2SpanIterator.next (DependencyLinkV2SpanIterator.java:88-159) on the device, the
+ * spans put trace by trace (traces = runs of equal trace_lo, as ByTraceId compares only the low
+ * 64 bits). Row columns may be host or device memory; synchronous.
+ * `service` = raw dictionary id of ENDPOINT_SERVICE_NAME (-1 = SQL null or ""): raw strings, since
+ * the "sa".equals("ca") check compares them before lower-casing; lower[raw] = the service id of
+ * the lower-cased name (Endpoint.Builder.serviceName), which the counts use. */
+#define ZDL_AKEY_NONE  0  /* a_key null or another key */
+#define ZDL_AKEY_LC    1
+#define ZDL_AKEY_CA    2
+#define ZDL_AKEY_CS    3
+#define ZDL_AKEY_SA    4
+#define ZDL_AKEY_SR    5
+#define ZDL_AKEY_ERROR 6
+typedef struct zdl_mysql_rows {
+  const uint64_t* trace_lo;   /* ZIPKIN_SPANS.TRACE_ID */
+  const uint64_t* trace_hi;   /* TRACE_ID_HIGH, may be NULL (only checked for the all-zero id) */
+  const uint64_t* span_id;    /* ZIPKIN_SPANS.ID */
+  const uint64_t* parent_id;  /* 0 = SQL null */
+  const uint8_t*  a_key;      /* ZDL_AKEY_* of ZIPKIN_ANNOTATIONS.A_KEY */
+  const int32_t*  a_type;     /* A_TYPE (V1BinaryAnnotation.TYPE_STRING = 6 marks an error tag) */
+  const int32_t*  service;    /* raw ENDPOINT_SERVICE_NAME id, -1 = null / empty */
+} zdl_mysql_rows;
+int         zdl_put_mysql_rows(zdl_ctx* ctx, const zdl_mysql_rows* rows, uint64_t n_rows,
+                               const int32_t* lower, uint32_t n_raw);
+const char* zdl_rows_last_error(void);  /* this thread's last zdl_put_mysql_rows failure */
+
 /* Kernel durations of the most recent put (+ link) when ZDL_FLAG_TIMING is set. */
 int zdl_get_kernel_times(zdl_ctx* ctx, zdl_kernel_times* out);
 

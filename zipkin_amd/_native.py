@@ -17,6 +17,7 @@ ZDL_ORDER_SORTED, ZDL_ORDER_FIRST_SEEN, ZDL_ORDER_INSERTION = 0, 1, 2
 ZDL_FLAG_TIMING = 1
 ZDL_FLAG_TIMING_ALL = 2
 ZDL_FLAG_INSERTION_ORDER = 4
+ZDL_AKEY_NONE, ZDL_AKEY_LC, ZDL_AKEY_CA, ZDL_AKEY_CS, ZDL_AKEY_SA, ZDL_AKEY_SR, ZDL_AKEY_ERROR = range(7)
 
 PF_KIND_SHIFT = 16
 PF_SHARED_SHIFT = 19
@@ -35,7 +36,7 @@ EXPORTS = (
     "zdl_store_size", "zdl_put_stored",
     "zdl_decoder_create", "zdl_decoder_destroy", "zdl_decoder_last_error", "zdl_decoder_bind",
     "zdl_decoder_dict_size", "zdl_decoder_missing", "zdl_decode_proto3", "zdl_decode_proto3_retry",
-    "zdl_decoder_download", "zdl_decoder_kernel_ms",
+    "zdl_decoder_download", "zdl_decoder_kernel_ms", "zdl_put_mysql_rows", "zdl_rows_last_error",
 )
 
 
@@ -59,6 +60,18 @@ class DayLinks(C.Structure):
     _fields_ = [("n_days", C.c_uint64), ("day_ms", C.POINTER(C.c_int64)), ("n", C.c_uint64),
                 ("day", C.POINTER(C.c_int64)), ("parent", C.POINTER(C.c_int32)), ("child", C.POINTER(C.c_int32)),
                 ("call_count", C.POINTER(C.c_int64)), ("error_count", C.POINTER(C.c_int64))]
+
+
+class MysqlRows(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ("trace_lo", "trace_hi", "span_id", "parent_id", "a_key", "a_type",
+                                          "service")]
+
+    @staticmethod
+    def arrays(hi, lo, pid, sid, key, typ, svc) -> dict:
+        return dict(trace_hi=np.asarray(hi, np.uint64), trace_lo=np.asarray(lo, np.uint64),
+                    parent_id=np.asarray(pid, np.uint64), span_id=np.asarray(sid, np.uint64),
+                    a_key=np.asarray(key, np.uint8), a_type=np.asarray(typ, np.int32),
+                    service=np.asarray(svc, np.int32))
 
 
 class Decoded(C.Structure):
@@ -146,6 +159,9 @@ def lib() -> C.CDLL:
     L.zdl_decode_proto3.argtypes = [vp, C.c_char_p, u64, C.POINTER(Decoded)]
     L.zdl_decode_proto3_retry.argtypes = [vp, C.POINTER(Decoded)]
     L.zdl_decoder_download.argtypes = [vp, C.POINTER(SpanCols)]
+    L.zdl_put_mysql_rows.argtypes = [vp, C.POINTER(MysqlRows), u64, vp, u32]
+    L.zdl_put_mysql_rows.restype = C.c_int
+    L.zdl_rows_last_error.restype = C.c_char_p
     L.zdl_decoder_kernel_ms.restype = C.c_float
     L.zdl_decoder_kernel_ms.argtypes = [vp]
     for name in ("zdl_decoder_bind", "zdl_decoder_missing", "zdl_decode_proto3", "zdl_decode_proto3_retry",
@@ -231,6 +247,19 @@ class Context:
 
     def sync(self):
         self.check(self._L.zdl_sync(self.h))
+
+    def put_mysql_rows(self, a: dict, lower: np.ndarray) -> None:
+        """zdl_put_mysql_rows over host row columns (MysqlRows.arrays)."""
+        a = {k: np.ascontiguousarray(v) for k, v in a.items()}
+        lw = np.ascontiguousarray(lower, np.int32)
+        r = MysqlRows(*(_ptr(a[k]) for k in ("trace_lo", "trace_hi", "span_id", "parent_id", "a_key", "a_type",
+                                             "service")))
+        rc = self._L.zdl_put_mysql_rows(self.h, C.byref(r), len(a["trace_lo"]), _ptr(lw), len(lw))
+        if rc != ZDL_OK:
+            msg = self._L.zdl_rows_last_error().decode()
+            if rc == ZDL_EREF_IAE:
+                raise ReferenceIllegalArgumentException(rc, msg)
+            raise ZdlError(rc, msg)
 
     @staticmethod
     def _links_to_numpy(out: Links):

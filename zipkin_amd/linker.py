@@ -94,6 +94,30 @@ class DependencyLinker:
         ctx.put_spans(cols)
         return self
 
+    def put_mysql_rows(self, rows) -> "DependencyLinker":
+        """AggregateDependencies.apply's putTrace loop over its cursor rows (mysql-v1
+        AggregateDependencies.java:71-84) with DependencyLinkV2SpanIterator's projection
+        (DependencyLinkV2SpanIterator.java:88-159) on the device (zdl_put_mysql_rows).
+
+        rows: (trace_id_high, trace_id, parent_id, id, a_key, a_type, endpoint_service_name)
+        tuples in the query's order (grouped by trace id, then span id); None = SQL null."""
+        rows = list(rows)
+        if not rows:
+            return self
+        m = (1 << 64) - 1
+        raw = Dictionary()
+        keys = {"lc": N.ZDL_AKEY_LC, "ca": N.ZDL_AKEY_CA, "cs": N.ZDL_AKEY_CS, "sa": N.ZDL_AKEY_SA,
+                "sr": N.ZDL_AKEY_SR, "error": N.ZDL_AKEY_ERROR}
+        cols = N.MysqlRows.arrays(
+            [(r[0] or 0) & m for r in rows], [(r[1] or 0) & m for r in rows], [(r[2] or 0) & m for r in rows],
+            [(r[3] or 0) & m for r in rows], [keys.get(r[4], N.ZDL_AKEY_NONE) for r in rows],
+            [r[5] if r[5] is not None else -1 for r in rows],
+            [raw.id(r[6]) if r[6] else -1 for r in rows])  # emptyToNull
+        # ep(name) lower-cases (Endpoint.Builder.serviceName); the raw ids keep "sa".equals("ca")
+        lower = np.array([self.svc.id(x.lower()) for x in raw.strings], np.int32)
+        self._context().put_mysql_rows(cols, lower)
+        return self
+
     def link(self) -> List[DependencyLink]:
         """link() (DependencyLinker.java:184)."""
         if self._ctx is None:
