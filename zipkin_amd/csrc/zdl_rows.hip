@@ -111,7 +111,9 @@ __global__ void k_row_project(Rows r, uint64_t n, const unsigned long long* pos,
   c.ip6[s] = -1;
   c.pf[s] = kind << ZDL_PF_KIND_SHIFT | (error ? ZDL_PF_ERROR : 0u);
   c.ts[s] = 0;
-  if (j == n) c.off[t + 1] = s + 1;  // the last span run closes the offsets
+  // the last span run closes the offsets; t counts the trace heads before row i, so a run that
+  // is not itself a trace head belongs to trace t - 1
+  if (j == n) c.off[(th ? t : t - 1) + 1] = s + 1;
 }
 
 template <class T>
