@@ -82,6 +82,47 @@ def proto3_leg(cols, w, S, device, doff, links, reps=5):
             "parity": "same links" if got == exp else "MISMATCH"}
 
 
+def mysql_rows_leg(cols, S, device, max_spans=2_000_000, reps=3):
+    """The first traces of the batch (<= max_spans spans) as mysql-v1 cursor rows (one row per
+    annotation a span would carry in v1: sr/ca for servers, cs/sa for clients, lc for local spans,
+    an error tag row) through zdl_put_mysql_rows + link: rows/s with the rows in host memory
+    (as a JDBC cursor delivers them), i.e. PCIe-inclusive. Timing only (parity: tests/)."""
+    from zipkin_amd import _native as N
+    k = int(np.searchsorted(cols.offsets, max_spans, side="right")) - 1
+    m = int(cols.offsets[k])
+    kind = (cols.port_flags[:m] >> 16) & 7
+    err = (cols.port_flags[:m] >> 21) & 1
+    loc, rem = cols.local_svc[:m], cols.remote_svc[:m]
+    key = np.zeros((m, 3), np.uint8)
+    svc = np.full((m, 3), -1, np.int32)
+    key[:, 0] = np.where(kind == 1, N.ZDL_AKEY_SR, np.where(kind == 0, N.ZDL_AKEY_CS, N.ZDL_AKEY_LC))
+    svc[:, 0] = loc
+    key[:, 1] = np.where(kind == 1, N.ZDL_AKEY_CA, np.where(kind == 0, N.ZDL_AKEY_SA, 0))
+    svc[:, 1] = np.where(key[:, 1] > 0, rem, -1)
+    key[:, 2] = np.where(err > 0, N.ZDL_AKEY_ERROR, 0)
+    svc[:, 2] = np.where(err > 0, loc, -1)
+    keep = ((key > 0) & (svc >= 0)).reshape(-1)
+    keep.reshape(m, 3)[:, 0] = True  # every span has its row (the left join)
+    span = np.repeat(np.arange(m), 3)[keep]
+    a = N.MysqlRows.arrays(np.zeros(len(span), np.uint64), cols.trace_lo[span], cols.parent_id[span],
+                           cols.id[span], key.reshape(-1)[keep], np.full(len(span), 6, np.int32),
+                           svc.reshape(-1)[keep])
+    lower = np.arange(S, dtype=np.int32)
+    ctx = N.Context(S, device=device)
+    ctx.put_mysql_rows(a, lower)  # warm
+    ts = []
+    for _ in range(reps):
+        ctx.reset()
+        t0 = time.perf_counter()
+        ctx.put_mysql_rows(a, lower)
+        ctx.link()
+        ts.append(time.perf_counter() - t0)
+    ctx.close()
+    t = float(np.median(ts))
+    return {"rows": int(len(span)), "spans": m, "traces": k, "ms": t * 1e3, "rows_per_s": len(span) / t,
+            "spans_per_s": m / t, "note": "rows host-resident (PCIe-inclusive), timing only"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -208,6 +249,10 @@ def main():
         p3 = proto3_leg(cols, w, S, local, doff, (p, c, n, e))
         log(f"proto3 ingest: kernel {p3['kernel_ms']:.3f} ms ({p3['kernel_gbs']:.0f} GB/s), "
             f"call {p3['call_ms']:.1f} ms, links {p3['parity']}")
+    rows_leg = None
+    if world == 1 and not args.no_proto3:
+        rows_leg = mysql_rows_leg(cols, S, local)
+        log(f"mysql rows: {rows_leg['rows']} rows in {rows_leg['ms']:.1f} ms ({rows_leg['rows_per_s']:.3e} rows/s)")
     parity = None
     cpu = None
     if rank == 0 and world == 1 and not args.no_parity:
@@ -277,7 +322,7 @@ def main():
                        "kernel_ms": {"k_link": tiles},
                        "step_roofline_frac": bytes_path / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
                        "parity": parity, "links": int(len(p)), "insertion_order": ins,
-                       "proto3_ingest": p3},
+                       "proto3_ingest": p3, "mysql_rows": rows_leg},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "k_link", "algorithmic_bytes_per_launch": bytes_launch},
