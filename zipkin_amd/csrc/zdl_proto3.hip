@@ -30,6 +30,7 @@
 #include <algorithm>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -531,7 +532,6 @@ struct zdl_decoder {
   DBuf<uint8_t> buf;
   DBuf<uint64_t> start;
   DBuf<uint32_t> slen;
-  HBuf<uint8_t> stage;  // pinned copy of the batch: the upload source, and where missing keys are read
   std::vector<uint64_t> start_h;
   std::vector<uint32_t> slen_h;
   uint64_t len = 0, n = 0;
@@ -634,6 +634,9 @@ int run_kernel(zdl_decoder* d, zdl_decoded* out) {
     DEC_TRY(d, hipMemcpyAsync(m.data(), d->miss.p, n, hipMemcpyDeviceToHost, s));
     DEC_TRY(d, hipMemcpyAsync(mo.data(), d->miss_off.p, 4 * n * 8, hipMemcpyDeviceToHost, s));
     DEC_TRY(d, hipMemcpyAsync(ml.data(), d->miss_len.p, 4 * n * 4, hipMemcpyDeviceToHost, s));
+    // the raw key bytes: the batch back from HBM (only on a pass with misses, i.e. new keys)
+    std::vector<uint8_t> raw(d->len);
+    DEC_TRY(d, hipMemcpyAsync(raw.data(), d->buf.p, d->len, hipMemcpyDeviceToHost, s));
     DEC_TRY(d, hipStreamSynchronize(s));
     d->missing.clear();
     std::unordered_map<std::string, bool> seen;
@@ -646,7 +649,7 @@ int run_kernel(zdl_decoder* d, zdl_decoded* out) {
         if (sl == SLOT_LIP4) {
           for (int b = 3; b >= 0; --b) k.push_back((char)(uint8_t)(off >> (8 * b)));
         } else {
-          k.append((const char*)d->stage.p + off, ml[4 * i + sl]);
+          k.append((const char*)raw.data() + off, ml[4 * i + sl]);
         }
         if (seen.emplace(k, true).second) d->missing.push_back(k);
       }
@@ -730,41 +733,46 @@ int zdl_decode_proto3(zdl_decoder* d, const uint8_t* data, uint64_t len, zdl_dec
   (void)hipGetLastError();
   DEC_TRY(d, hipSetDevice(d->device));
   d->missing.clear();
-  // top-level scan: Proto3Codec.readList / SpanField.read (key tossed) / readLengthPrefix
+  const hipStream_t s = d->stream;
+  // the batch goes up straight from the caller's bytes while a host thread runs the top-level
+  // scan (Proto3Codec.readList / SpanField.read: key tossed / readLengthPrefix) over them
   d->start_h.clear();
   d->slen_h.clear();
   d->scan_rc = len == 0 ? 1 : ZDL_OK;  // empty input -> false -> emptyList
-  uint64_t pos = 0;
-  while (d->scan_rc == ZDL_OK && pos < len) {
-    int32_t key, n;
-    if (!host_varint32(data, len, pos, key) || !host_varint32(data, len, pos, n) || (int64_t)n > (int64_t)(len - pos)) {
-      d->scan_rc = ZDL_EREF_IAE;
-      break;
+  std::thread scan([d, data, len] {
+    uint64_t pos = 0;
+    while (d->scan_rc == ZDL_OK && pos < len) {
+      int32_t key, n;
+      if (!host_varint32(data, len, pos, key) || !host_varint32(data, len, pos, n) ||
+          (int64_t)n > (int64_t)(len - pos)) {
+        d->scan_rc = ZDL_EREF_IAE;
+        break;
+      }
+      if (n == 0) {
+        d->scan_rc = 1;
+        break;
+      }
+      if (n < 0) {  // readValue(negative) ends before it starts: the lenient case (unsupported)
+        d->scan_rc = ZDL_EINVAL;
+        break;
+      }
+      d->start_h.push_back(pos);
+      d->slen_h.push_back((uint32_t)n);
+      pos += (uint64_t)n;
     }
-    if (n == 0) {
-      d->scan_rc = 1;
-      break;
-    }
-    if (n < 0) {  // readValue(negative) ends before it starts: the lenient case (unsupported)
-      d->scan_rc = ZDL_EINVAL;
-      break;
-    }
-    d->start_h.push_back(pos);
-    d->slen_h.push_back((uint32_t)n);
-    pos += (uint64_t)n;
-  }
+  });
+  hipError_t up = d->buf.ensure(len);
+  if (up == hipSuccess && len) up = hipMemcpyAsync(d->buf.p, data, len, hipMemcpyHostToDevice, s);
+  if (up == hipSuccess) up = hipStreamSynchronize(s);  // `data` is borrowed for this call only
+  scan.join();
+  DEC_TRY(d, up);
   if (d->start_h.size() >= (1ull << 31)) return dfail(d, ZDL_EINVAL, "zdl_decode_proto3: at most 2^31 spans per batch");
   const uint64_t n = d->start_h.size();
   d->n = n;
   d->len = len;
-  const hipStream_t s = d->stream;
   if (n) {
-    DEC_TRY(d, d->stage.ensure(len));
-    std::memcpy(d->stage.p, data, len);
-    DEC_TRY(d, d->buf.ensure(len));
     DEC_TRY(d, d->start.ensure(n));
     DEC_TRY(d, d->slen.ensure(n));
-    DEC_TRY(d, hipMemcpyAsync(d->buf.p, d->stage.p, len, hipMemcpyHostToDevice, s));
     DEC_TRY(d, hipMemcpyAsync(d->start.p, d->start_h.data(), n * 8, hipMemcpyHostToDevice, s));
     DEC_TRY(d, hipMemcpyAsync(d->slen.p, d->slen_h.data(), n * 4, hipMemcpyHostToDevice, s));
     DEC_TRY(d, d->lo.ensure(n));
