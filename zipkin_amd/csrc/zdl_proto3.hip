@@ -85,16 +85,19 @@ enum : int { F_OK = 0, F_IAE = 1, F_OVERRUN = 2 };
 
 // Buffer over the whole batch (bounds = the batch, as in Buffer.java); fail is sticky. Bytes
 // inside the block's LDS window [w0, w0 + wn) are read from LDS, the rest from HBM.
+typedef __attribute__((address_space(3))) const uint8_t lds_u8;  // ds_read, not flat loads
+
 struct Rd {
   const uint8_t* b;
   uint64_t n, pos;
   int fail;
-  const uint8_t* w;
+  lds_u8* w;
   uint64_t w0, wn;
 
   __device__ __forceinline__ uint8_t at(uint64_t p) const {
     const uint64_t q = p - w0;
-    return q < wn ? w[q] : b[p];
+    if (q < wn) return w[(uint32_t)q];
+    return b[p];
   }
   __device__ __forceinline__ uint8_t byte() {
     if (pos >= n) {
@@ -289,7 +292,7 @@ __global__ void __launch_bounds__(kBlock) k_proto3_spans(const uint8_t* __restri
   __syncthreads();
   const uint32_t i = first + threadIdx.x;
   if (i >= n) return;
-  Rd r{buf, len, start[i], F_OK, win, w0, wn};
+  Rd r{buf, len, start[i], F_OK, (lds_u8*)win, w0, wn};
   const int64_t end = (int64_t)(r.pos + slen[i]);
   bool has_trace = false, has_id = false, shared = false, error = false;
   uint64_t lo = 0, id = 0, pid = 0;
