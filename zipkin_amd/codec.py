@@ -88,3 +88,46 @@ def link_to_json(l: DependencyLink) -> Dict[str, Any]:
 
 def link_from_json(d: Dict[str, Any]) -> DependencyLink:
     return DependencyLink.create(d["parent"], d["child"], d.get("callCount", 0), d.get("errorCount", 0))
+
+
+# JsonEscaper.REPLACEMENT_CHARS (zipkin2/internal/JsonEscaper.java): every control
+# character as \u00xx, then the short forms for quote, backslash, \t \b \n \r \f.
+_JSON_REPLACEMENTS = {i: "\\u%04x" % i for i in range(0x20)}
+_JSON_REPLACEMENTS.update({ord('"'): '\\"', ord("\\"): "\\\\", ord("\t"): "\\t", ord("\b"): "\\b",
+                           ord("\n"): "\\n", ord("\r"): "\\r", ord("\f"): "\\f",
+                           0x2028: "\\u2028", 0x2029: "\\u2029"})
+
+
+def json_escape(v: str) -> str:
+    """JsonEscaper.jsonEscape: RFC 7159 escapes plus U+2028 / U+2029."""
+    return v.translate(_JSON_REPLACEMENTS)
+
+
+def _utf8(v: str) -> bytes:
+    # Buffer.writeUtf8 writes '?' for an unpaired surrogate.
+    return v.encode("utf-8", "replace")
+
+
+def encode_link(l: DependencyLink) -> bytes:
+    """DependencyLinkBytesEncoder.JSON_V1.encode (DependencyLinkBytesEncoder.java:35-65).
+
+    ``{"parent":"…","child":"…","callCount":N[,"errorCount":E]}``, errorCount only when > 0,
+    no whitespace; the same bytes the reference's ``/api/v2/dependencies`` returns per link.
+    """
+    out = b'{"parent":"' + _utf8(json_escape(l.parent)) + b'","child":"' + _utf8(json_escape(l.child))
+    out += b'","callCount":' + str(int(l.call_count)).encode()
+    if l.error_count > 0:
+        out += b',"errorCount":' + str(int(l.error_count)).encode()
+    return out + b"}"
+
+
+def encode_links(links) -> bytes:
+    """DependencyLinkBytesEncoder.JSON_V1.encodeList via JsonCodec.writeList (JsonCodec.java:206-232)."""
+    return b"[" + b",".join(encode_link(l) for l in links) + b"]"
+
+
+def decode_links(data) -> List[DependencyLink]:
+    """DependencyLinkBytesDecoder.JSON_V1.decodeList: the inverse of :func:`encode_links`."""
+    if isinstance(data, (bytes, bytearray)):
+        data = data.decode("utf-8")
+    return [link_from_json(d) for d in json.loads(data)]
