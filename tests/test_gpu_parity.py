@@ -48,6 +48,18 @@ def test_golden_dependency_linker(case):
     linker.close()
 
 
+@pytest.mark.parametrize("case", [c for c in DL["cases"] if c["mode"] == "exact"],
+                         ids=lambda c: c["name"])
+def test_golden_response_bytes(case):
+    """The JSON_V1 bytes of the device's links equal those of the expected links, in order."""
+    from zipkin_amd.codec import encode_links
+    linker = DependencyLinker()
+    for t in case["traces"]:
+        linker.put_trace(spans(t))
+    assert encode_links(linker.link()) == encode_links(links(case["expect"]))
+    linker.close()
+
+
 @pytest.mark.parametrize("case", DL["merge_cases"], ids=lambda c: c["name"])
 def test_golden_merge_exact_order(case):
     check_links(DependencyLinker.merge(links(case["links"])), case["expect"], case["mode"])
