@@ -134,6 +134,7 @@ def main():
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--cpu-sample-traces", type=int, default=200_000)
     ap.add_argument("--no-proto3", action="store_true", help="skip the proto3 ingest side leg")
+    ap.add_argument("--no-mysql-rows", action="store_true", help="skip the mysql-v1 rows side leg")
     ap.add_argument("--no-insertion-order", action="store_true",
                     help="skip the side measurement of the insertion-order mode (N = 1 only)")
     args = ap.parse_args()
@@ -250,7 +251,7 @@ def main():
         log(f"proto3 ingest: kernel {p3['kernel_ms']:.3f} ms ({p3['kernel_gbs']:.0f} GB/s), "
             f"call {p3['call_ms']:.1f} ms, links {p3['parity']}")
     rows_leg = None
-    if world == 1 and not args.no_proto3:
+    if world == 1 and not args.no_mysql_rows:
         rows_leg = mysql_rows_leg(cols, S, local)
         log(f"mysql rows: {rows_leg['rows']} rows in {rows_leg['ms']:.1f} ms ({rows_leg['rows_per_s']:.3e} rows/s)")
     parity = None
