@@ -5,11 +5,19 @@ reset the S x S counts, zdl_put_spans_device (k_link, k_link_full, k_big), for N
 one RCCL all-reduce of the count tables, then zdl_link (ordered compaction into mapped
 pinned memory, one sync) -> the DependencyLink list.
 
-N = 1 runs C2 (10M spans / 1M traces / 50 services). N > 1 is weak scaling:
-every rank links its own C2-sized shard of traces picked by
-splitmix64(trace_lo) % N, and the ranks sum their tables once (RCCL over xGMI).
+N = 1 runs C2 (10M spans / 1M traces / 50 services), BASELINE.json configs[1]. N > 1 is
+weak scaling on C3's shape (500 services): every rank links its own C3 per-GPU shard
+(12.5M traces = 125M spans, the 1B / 8 split) of traces picked by splitmix64(trace_lo) % N,
+and the ranks sum their tables once (RCCL over xGMI). `--config c3` runs that shard at N = 1.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c4|c5]
+Roofline accounting follows SURVEY.md §8(d) / BASELINE.md: algorithmic bytes
+W = 44 B/span (trace_lo, id, parent_id, 4 dictionary ids, port_flags) + 8 B/trace (CSR
+offset). `roofline` prices the dominant kernel (k_link, HIP events on the context stream)
+with W; `config.step_roofline_frac` prices the whole device step (reset, kernels, combine,
+link) with W; `config.k_link_read_frac` uses the 36 B/span k_link actually reads (the CSR
+grouping replaces trace_lo).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5]
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 """
 from __future__ import annotations
@@ -27,8 +35,10 @@ sys.path.insert(0, ROOT)
 
 METRIC = "spans/sec linked to DependencyLinks at 1/2/4/8 MI355X; % of HBM roofline"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
-BYTES_PER_SPAN = 36            # id 8 + parent_id 8 + 4 x i32 dictionary ids + port_flags 4 (k_link)
+BYTES_PER_SPAN = 44            # trace_lo 8 + id 8 + parent_id 8 + 4 x i32 ids + port_flags 4
+READ_BYTES_PER_SPAN = 36       # what k_link reads: the CSR grouping stands in for trace_lo
 BYTES_PER_TRACE = 8            # CSR offset (k_link plans its windows from them)
+C3_TRACES_PER_GPU = 12_500_000  # C3's 100M traces over 8 GPUs
 
 
 def log(*a):
@@ -123,16 +133,87 @@ def mysql_rows_leg(cols, S, device, max_spans=2_000_000, reps=3):
             "spans_per_s": m / t, "note": "rows host-resident (PCIe-inclusive), timing only"}
 
 
+def cpu_info():
+    """The host cores this process may run on: affinity mask, capped by a cgroup CPU quota
+    (the GPU box shares its host: nproc shows the whole machine), plus the CPU model."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = nproc
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    usable = aff if quota is None else max(1, min(aff, int(quota)))
+    env = os.environ.get("OMP_NUM_THREADS")
+    why = f"affinity {aff} of nproc {nproc}" + (f", cgroup quota {quota:g} CPUs" if quota else ", no cgroup quota")
+    if env and env.isdigit() and int(env) < usable:
+        usable = int(env)
+        why += f", OMP_NUM_THREADS={env} (the box's CPU share)"
+    model = "unknown"
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"nproc": nproc, "affinity": aff, "quota": quota, "usable": usable, "model": model, "why": why}
+
+
+def h2d_leg(cols, S, device, reps=3):
+    """Host-buffer side of the path (not `value`): the batch's 44 B/span columns + offsets
+    copied from pinned host memory (the PCIe rate a JNI caller with pinned buffers gets), and
+    a whole zdl_put_spans + zdl_link from pageable numpy columns (pack excluded)."""
+    import torch
+    from zipkin_amd import _native as N
+    names = ("trace_lo", "id", "parent_id", "local_svc", "remote_svc", "local_ip4", "local_ip6", "port_flags")
+    host = [torch.from_numpy(np.ascontiguousarray(getattr(cols, k)).view(
+        np.int64 if getattr(cols, k).dtype.itemsize == 8 else np.int32)).pin_memory() for k in names]
+    host.append(torch.from_numpy(cols.offsets.view(np.int64)).pin_memory())
+    dev = torch.device("cuda", device)
+    outs = [torch.empty_like(h, device=dev) for h in host]
+    nbytes = sum(h.numel() * h.element_size() for h in host)
+    ts = []
+    for _ in range(reps + 1):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for h, o in zip(host, outs):
+            o.copy_(h, non_blocking=True)
+        torch.cuda.synchronize(dev)
+        ts.append(time.perf_counter() - t0)
+    h2d = float(np.median(ts[1:]))
+    ctx = N.Context(S, device=device)
+    es = []
+    for _ in range(reps + 1):
+        ctx.reset()
+        t0 = time.perf_counter()
+        ctx.put_spans(cols)
+        ctx.link()
+        es.append(time.perf_counter() - t0)
+    ctx.close()
+    e2e = float(np.median(es[1:]))
+    del outs, host
+    return {"bytes": nbytes, "h2d_ms": h2d * 1e3, "h2d_gbs": nbytes / h2d / 1e9, "e2e_ms": e2e * 1e3,
+            "e2e_spans_per_s": cols.n_spans / e2e,
+            "note": "h2d: pinned host -> HBM copy of the 44 B/span columns; e2e: zdl_put_spans (pageable host "
+                    "columns, staged copies) + zdl_link, PCIe-inclusive"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c2")
+    ap.add_argument("--config", default=None, help="default: c2 at N = 1, c3 (per-GPU shard) at N > 1")
     ap.add_argument("--traces", type=int, default=0, help="override traces per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
-    ap.add_argument("--cpu-sample-traces", type=int, default=200_000)
+    ap.add_argument("--no-h2d", action="store_true", help="skip the host-buffer (PCIe-inclusive) leg")
     ap.add_argument("--no-proto3", action="store_true", help="skip the proto3 ingest side leg")
     ap.add_argument("--no-mysql-rows", action="store_true", help="skip the mysql-v1 rows side leg")
     ap.add_argument("--no-insertion-order", action="store_true",
@@ -156,7 +237,10 @@ def main():
         dist.init_process_group("nccl", init_method="env://")
     dev = torch.device("cuda", local)
 
-    w = synth.CONFIGS[args.config]
+    config = args.config or ("c2" if world == 1 else "c3")
+    w = synth.CONFIGS[config]
+    if config == "c3":  # weak scaling: one C3 per-GPU shard per rank
+        w = w.scaled(C3_TRACES_PER_GPU)
     if args.traces:
         w = w.scaled(args.traces)
     if world > 1:
@@ -225,7 +309,8 @@ def main():
     # link() is DependencyLinker.link()'s list order (k_link plans, k_tail links exactly)
     ins = None
     ins_out = None
-    if world == 1 and not args.no_insertion_order:
+    side = world == 1 and config == "c2"  # the side legs run on C2 only
+    if side and not args.no_insertion_order:
         ictx = N.Context(S, device=local, insertion_order=True)
 
         def istep():
@@ -246,19 +331,25 @@ def main():
     # side measurement (not `value`): the same batch as a proto3 ListOfSpans decoded on the device
     # (zdl_decode_proto3) and linked from the decoded HBM columns
     p3 = None
-    if world == 1 and not args.no_proto3:
+    if side and not args.no_proto3:
         p3 = proto3_leg(cols, w, S, local, doff, (p, c, n, e))
         log(f"proto3 ingest: kernel {p3['kernel_ms']:.3f} ms ({p3['kernel_gbs']:.0f} GB/s), "
             f"call {p3['call_ms']:.1f} ms, links {p3['parity']}")
     rows_leg = None
-    if world == 1 and not args.no_mysql_rows:
+    if side and not args.no_mysql_rows:
         rows_leg = mysql_rows_leg(cols, S, local)
         log(f"mysql rows: {rows_leg['rows']} rows in {rows_leg['ms']:.1f} ms ({rows_leg['rows_per_s']:.3e} rows/s)")
+    h2d = None
+    if side and not args.no_h2d:
+        h2d = h2d_leg(cols, S, local)
+        log(f"host buffers: H2D {h2d['h2d_ms']:.2f} ms ({h2d['h2d_gbs']:.1f} GB/s pinned), put+link from pageable "
+            f"host columns {h2d['e2e_ms']:.2f} ms")
     parity = None
     cpu = None
     if rank == 0 and world == 1 and not args.no_parity:
         from oracle import ref
-        threads = min(os.cpu_count() or 1, 16)
+        ci = cpu_info()
+        threads = ci["usable"]
         t1 = time.perf_counter()
         st, op, oc, on, oe = ref.link(cols, threads=threads)
         t_multi = time.perf_counter() - t1
@@ -273,28 +364,25 @@ def main():
             log(f"insertion order: {ins['ms_per_step']:.2f} ms/step, {ins['parity']}")
         log(f"parity vs C++ restatement ({threads} threads, {t_multi:.2f}s): {parity}, {len(got)} links")
         if not args.no_cpu_baseline:
-            k = min(args.cpu_sample_traces, cols.n_traces)
-            m = int(cols.offsets[k])
-            from zipkin_amd.columnar import Columns
-            sample = Columns(*(getattr(cols, f)[:m] for f in ("trace_lo", "id", "parent_id", "local_svc",
-                                                                "remote_svc", "local_ip4", "local_ip6",
-                                                                "port_flags", "timestamp")),
-                             np.ascontiguousarray(cols.offsets[:k + 1]))
+            # the whole batch on one thread = one DependencyLinker over every trace
             t1 = time.perf_counter()
-            ref.link(sample, threads=1)
+            ref.link(cols, threads=1)
             t_one = time.perf_counter() - t1
-            cpu = {"value": m / t_one, "unit": "spans/s", "cores": 1, "kind": "port",
-                   "sample": f"first {k} traces ({m} spans) of the same C2 batch, 1 thread = one "
-                             f"DependencyLinker (C++ restatement of the reference algorithm)",
-                   "multi_thread": {"value": cols.n_spans / t_multi, "cores": threads,
-                                    "sample": "whole batch, trace-sharded linkers + merge"}}
-            log(f"cpu baseline: {m / t_one:.3e} spans/s on 1 thread; {cols.n_spans / t_multi:.3e} on {threads}")
+            cpu = {"value": cols.n_spans / t_multi, "unit": "spans/s", "cores": threads, "kind": "port",
+                   "sample": f"the whole {w.name} batch ({cols.n_spans} spans), trace-sharded C++ restatement "
+                             f"of DependencyLinker (one linker per thread + DependencyLinker.merge) on {threads} "
+                             f"threads = every core this process may use ({ci['why']})",
+                   "cpu": ci, "seconds": t_multi,
+                   "single_thread": {"value": cols.n_spans / t_one, "cores": 1, "seconds": t_one,
+                                     "sample": "the same batch through one linker, 1 thread"}}
+            log(f"cpu baseline: {cols.n_spans / t_one:.3e} spans/s on 1 thread; {cols.n_spans / t_multi:.3e} on "
+                f"{threads} ({ci['model']})")
 
     if rank == 0:
         ms_step = elapsed / args.steps * 1e3
-        # what k_link must read: every span once and every trace offset once
+        # every span once (44 B) and every trace offset once
         bytes_launch = BYTES_PER_SPAN * cols.n_spans + BYTES_PER_TRACE * (cols.n_traces + 1)
-        bytes_path = bytes_launch
+        read_launch = READ_BYTES_PER_SPAN * cols.n_spans + BYTES_PER_TRACE * (cols.n_traces + 1)
         achieved = bytes_launch / (tiles * 1e-3) / 1e9
         traffic = None
         pmc = os.path.join(ROOT, "profiles", "pmc_k_link.json")
@@ -321,12 +409,14 @@ def main():
             "config": {"workload": w.name, "spans_per_gpu": cols.n_spans, "traces_per_gpu": cols.n_traces,
                        "services": S, "parallelism": f"trace-shard x{world}" + (" + RCCL all-reduce" if world > 1 else ""),
                        "kernel_ms": {"k_link": tiles},
-                       "step_roofline_frac": bytes_path / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                       "parity": parity, "links": int(len(p)), "insertion_order": ins,
+                       "step_roofline_frac": bytes_launch / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                       "k_link_read_frac": read_launch / (tiles * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                       "parity": parity, "links": int(len(p)), "insertion_order": ins, "host_buffers": h2d,
                        "proto3_ingest": p3, "mysql_rows": rows_leg},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_link", "algorithmic_bytes_per_launch": bytes_launch},
+                         "kernel": "k_link", "algorithmic_bytes_per_launch": bytes_launch,
+                         "bytes_per_span": BYTES_PER_SPAN, "bytes_per_trace": BYTES_PER_TRACE},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

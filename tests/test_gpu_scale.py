@@ -1,0 +1,129 @@
+"""Every BASELINE config on the engine at its defining scale, against the C++ restatement
+(oracle/dl_ref.cpp), bit-exact on every (parent, child, callCount, errorCount):
+
+* C3: a per-GPU shard shape (500 services, C2 shape, 1M traces = 10M spans) through the
+  raw context (sorted output) and through the facade's table capacity on an
+  insertion-order context (DependencyLinker.link()'s exact list order);
+* C5: the Pareto body plus unclipped giant traces of 60k-190k spans (depth 64,
+  fan-out <= 1000), which take k_tail's big-trace path;
+* the multi-GPU combine on one device: contexts over disjoint splitmix64(trace_lo) shards,
+  zdl_table_export -> sum -> zdl_table_import -> zdl_link equals one context over
+  everything (DependencyLinker.merge semantics, DependencyLinker.java:189-204).
+"""
+import numpy as np
+import pytest
+
+from oracle import ref
+from zipkin_amd import _native as N
+from zipkin_amd import shard, synth
+from zipkin_amd.columnar import concat_columns
+from zipkin_amd.linker import _capacity
+
+pytestmark = pytest.mark.gpu
+
+
+def _tuples(p, c, n, e):
+    return list(zip(p.tolist(), c.tolist(), n.tolist(), e.tolist()))
+
+
+def _oracle(cols, threads=16):
+    st, p, c, n, e = ref.link(cols, threads=threads)
+    assert st == 0
+    return _tuples(p, c, n, e)
+
+
+def test_c3_shard_sorted_vs_cpp():
+    w = synth.C3.scaled(1_000_000)
+    cols = synth.generate(w)
+    assert cols.n_spans > 9_000_000
+    ctx = N.Context(w.total_services)
+    ctx.put_spans(cols)
+    got = sorted(_tuples(*ctx.link()))
+    ctx.close()
+    exp = sorted(_oracle(cols))
+    assert len(exp) > 100_000
+    assert got == exp
+
+
+def test_c3_shard_facade_capacity_insertion_order_vs_cpp():
+    """The DependencyLinker facade's context for 500 services (capacity 768) on the
+    insertion-order path: the reference's list order, exactly."""
+    w = synth.C3.scaled(1_000_000)
+    cols = synth.generate(w)
+    cap = _capacity(w.total_services)
+    assert cap > w.total_services
+    ctx = N.Context(cap, insertion_order=True)
+    ctx.put_spans(cols)
+    got = _tuples(*ctx.link(N.ZDL_ORDER_INSERTION))
+    ctx.close()
+    assert got == _oracle(cols)
+
+
+def _c5_with_giants():
+    body = synth.generate(synth.C5.scaled(300_000))
+    giants = []
+    for k, size in enumerate((60_000, 120_000, 190_000)):
+        g = synth.Workload(f"c5_giant_{k}", 0x5EED0050 + k, 1, 10_000, max_depth=64, size_dist=2,
+                           max_size=size, max_fanout=1000, zipf_s=1.1)
+        giants.append(synth.generate(g))
+    # giants first, in the middle and last: each sits in a different wave's chunk
+    h = body.n_traces // 2
+    first = _slice_traces(body, 0, h)
+    second = _slice_traces(body, h, body.n_traces)
+    return concat_columns([giants[0], first, giants[1], second, giants[2]])
+
+
+def _slice_traces(cols, t0, t1):
+    from zipkin_amd.columnar import Columns
+    a, b = int(cols.offsets[t0]), int(cols.offsets[t1])
+    f = ("trace_lo", "id", "parent_id", "local_svc", "remote_svc", "local_ip4", "local_ip6", "port_flags",
+         "timestamp")
+    return Columns(*(np.ascontiguousarray(getattr(cols, n)[a:b]) for n in f),
+                   np.ascontiguousarray(cols.offsets[t0:t1 + 1] - np.uint64(a)))
+
+
+def test_c5_unclipped_giant_traces_vs_cpp():
+    cols = _c5_with_giants()
+    sizes = np.diff(cols.offsets.astype(np.int64))
+    assert (sizes >= 50_000).sum() >= 3 and sizes.max() <= 200_000
+    ctx = N.Context(10_000)
+    ctx.put_spans(cols)
+    got = sorted(_tuples(*ctx.link()))
+    ctx.close()
+    assert got == sorted(_oracle(cols))
+
+
+@pytest.mark.parametrize("config", ["c4", "c3"])
+def test_two_shard_table_combine_on_one_device(config):
+    """bench.py's multi-GPU step on one device: per-shard contexts, their S x S tables
+    exported, summed (what the RCCL all-reduce does across ranks), imported, linked."""
+    import torch
+    w = synth.CONFIGS[config].scaled(200_000)
+    cols = synth.generate(w)
+    S = w.total_services
+    parts = shard.partition_columns(cols, 2)
+    assert all(p.n_spans > 0 for p in parts)
+    dev = torch.device("cuda", 0)
+    tables = []
+    for p in parts:
+        ctx = N.Context(S)
+        ctx.put_spans(p)
+        tc = torch.zeros(S * S, dtype=torch.int64, device=dev)
+        te = torch.zeros(S * S, dtype=torch.int64, device=dev)
+        ctx.table_export(tc.data_ptr(), te.data_ptr())
+        ctx.sync()
+        ctx.close()
+        tables.append((tc, te))
+    call = tables[0][0] + tables[1][0]
+    err = tables[0][1] + tables[1][1]
+    torch.cuda.synchronize(dev)
+    ctx = N.Context(S)
+    ctx.table_import(call.data_ptr(), err.data_ptr())
+    got = sorted(_tuples(*ctx.link()))
+    ctx.close()
+    one = N.Context(S)
+    one.put_spans(cols)
+    whole = sorted(_tuples(*one.link()))
+    one.close()
+    assert got == whole
+    assert got == sorted(_oracle(cols))

@@ -122,6 +122,7 @@ struct Gen {
   explicit Gen(const zdl_synth_params& p) : P(p) { zipf.init(std::max<uint32_t>(p.n_services, 1), p.zipf_s); }
 
   uint32_t trace_size(Rng& r) const {
+    if (P.size_dist == 2) return std::max<uint32_t>(1, P.max_size);  // every trace exactly max_size spans
     if (P.size_dist == 1) {
       const double u = 1.0 - r.uni();
       double x = std::pow(u, -1.0 / P.pareto_alpha);

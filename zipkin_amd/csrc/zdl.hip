@@ -533,13 +533,17 @@ __global__ void __launch_bounds__(TAIL_WG, 1) k_tail(Args A) {
   __syncthreads();
   big_traces<ORD>(A);
   if (!A.map) return;
-  // The table and status atomics are performed at the device-coherent level; waiting for
-  // this workgroup's to complete (vmcnt) before counting it done is enough, and the last
-  // workgroup reads the cells with device-coherent loads. (Agent-scope fences here cost an
-  // L2 writeback / invalidate per workgroup: 37 us measured.)
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  // Hand-off to the last workgroup (MI355X_MICROARCH.md, "Valid forms", first table row):
+  // the table and status updates are agent-scope atomics, performed at the memory side;
+  // every wave waits for its own to be acknowledged (vmcnt(0), written as inline asm: a
+  // workgroup-scope fence lowers to no wait outside TgSplit mode), then one lane per
+  // workgroup adds to `done`, and the workgroup whose add returns the last ticket reads
+  // the cells with sc1 (agent-scope) loads only. No agent-scope fence: that would write
+  // back the XCD's L2 per workgroup (37 us measured) and protects nothing here.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) last = atomicAdd(A.done, 1u) == gridDim.x - 1;
+  if (threadIdx.x == 0)
+    last = __hip_atomic_fetch_add(A.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   __syncthreads();
   if (!last) return;
   compact_ordered(A.call, A.err, A.rows * A.S, A.S, A.status, A.map);
@@ -699,6 +703,7 @@ struct zdl_ctx {
   unsigned long long* h_map = nullptr;  // mapped pinned: status, count, ordered records
   unsigned long long* d_map = nullptr;  // its device address
   bool map_fresh = false;               // h_map holds the compaction of the current table
+  bool poisoned = false;                // a put stopped between its kernels: zdl_reset required
   unsigned long long* h_flag = nullptr;  // mapped pinned: the last put's k_tail stores its seq
   unsigned long long* d_flag = nullptr;
   unsigned long long seq = 0;            // puts that compacted into h_map
@@ -1006,6 +1011,7 @@ static hipError_t ensure_map(zdl_ctx* c) {
 // compacts the table into the mapped buffer zdl_link reads.
 static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans, const uint64_t* off,
                           uint64_t n_traces, const uint64_t* n_traces_dev = nullptr) {
+  if (c->poisoned) return fail(c, ZDL_EDEVICE, "an earlier put failed between its kernels: call zdl_reset");
   const size_t SS = (size_t)c->rows * c->S;  // table cells (days * S * S with daily buckets)
   const int dense = SS <= (size_t)WDENSE_MAX;
   const int grid = c->grid, lgrid = c->cus * lk::wgs_per_cu;  // k_link: two 16-wave workgroups per CU
@@ -1044,15 +1050,8 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   A.cx_win = c->cx_win.p;
   A.skip = c->skip;
   A.prof = c->prof.p;
-  void* kargs[] = {&A};
-  ev_record(c, 0);
-  ev_record(c, 1);
-  const int lmode = (c->ord || c->days) ? 3 : (c->prof_on ? 1 : (c->skip ? 2 : 0));
-  HIP_TRY(c, hipLaunchKernel(k_link_fn(dense, c->window, lmode), dim3(lgrid),
-                             dim3(lk::waves(c->window) * 64), kargs, link_block_bytes(c->window), c->stream));
-  ev_record(c, 7);
-  ev_record(c, 2);
-  ev_record(c, 3);
+  // Every buffer of the put is allocated before its first kernel is launched: a failed
+  // allocation then leaves the tables, the counter slots and the epoch untouched.
   HIP_TRY(c, c->b_id.ensure(n_spans));
   HIP_TRY(c, c->b_pid.ensure(n_spans));
   HIP_TRY(c, c->b_lsvc.ensure(n_spans));
@@ -1093,10 +1092,28 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   A.done = c->counters.p + 4;
   if (A.map) {
     A.flag = c->d_flag;
-    A.seq = ++c->seq;
+    A.seq = c->seq + 1;
   }
-  HIP_TRY(c, hipLaunchKernel(k_tail_fn(dense, wmode, c->ord ? 1 : 0), dim3(grid), dim3(TAIL_WG), kargs,
-                             tail_block_bytes(wmode), c->stream));
+  void* kargs[] = {&A};
+  ev_record(c, 0);
+  ev_record(c, 1);
+  const int lmode = (c->ord || c->days) ? 3 : (c->prof_on ? 1 : (c->skip ? 2 : 0));
+  // A failed launch poisons nothing yet either: no kernel of this put ran
+  HIP_TRY(c, hipLaunchKernel(k_link_fn(dense, c->window, lmode), dim3(lgrid),
+                             dim3(lk::waves(c->window) * 64), kargs, link_block_bytes(c->window), c->stream));
+  ev_record(c, 7);
+  ev_record(c, 2);
+  ev_record(c, 3);
+  c->map_fresh = false;  // k_link has changed the table
+  const hipError_t le = hipLaunchKernel(k_tail_fn(dense, wmode, c->ord ? 1 : 0), dim3(grid), dim3(TAIL_WG), kargs,
+                                        tail_block_bytes(wmode), c->stream);
+  if (le != hipSuccess) {
+    // k_link ran but k_tail did not: the counter slots are not re-zeroed and the table
+    // holds part of the put. Mark the context: every put and link fails until zdl_reset.
+    c->poisoned = true;
+    return hip_fail(c, le, "k_tail launch");
+  }
+  if (A.map) c->seq = A.seq;
   c->span_base += n_spans;  // the next put's traces come after this one's
   ev_record(c, 4);
   ++c->epoch;  // k_tail zeroed the other counter slots
@@ -1382,6 +1399,10 @@ int zdl_put_spans(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans, const 
 int zdl_reset(zdl_ctx* c) {
   if (!c) return ZDL_EINVAL;
   HIP_TRY(c, enter(c));
+  if (c->poisoned) {  // the counter slots may hold a half-finished put's counts
+    HIP_TRY(c, hipMemsetAsync(c->counters.p, 0, 20, c->stream));
+    c->poisoned = false;
+  }
   const size_t SS = (size_t)c->rows * c->S;
   hipLaunchKernelGGL(k_zero_tables, dim3((unsigned)((SS + 255) / 256)), dim3(256), 0, c->stream, c->call.p,
                      c->errc.p, (uint64_t)SS, c->status.p, c->ord ? c->first.p : nullptr);
@@ -1468,6 +1489,7 @@ static int link_insertion(zdl_ctx* c, zdl_links* out) {
 int zdl_link(zdl_ctx* c, int order, zdl_links* out) {
   if (!c || !out) return ZDL_EINVAL;
   if (c->days) return fail(c, ZDL_EINVAL, "daily buckets are set: use zdl_link_days");
+  if (c->poisoned) return fail(c, ZDL_EDEVICE, "an earlier put failed between its kernels: call zdl_reset");
   if (order == ZDL_ORDER_INSERTION) {
     if (!c->ord) return fail(c, ZDL_EINVAL, "ZDL_ORDER_INSERTION needs a ZDL_FLAG_INSERTION_ORDER context");
     HIP_TRY(c, enter(c));
