@@ -127,3 +127,72 @@ def test_two_shard_table_combine_on_one_device(config):
     one.close()
     assert got == whole
     assert got == sorted(_oracle(cols))
+
+
+@pytest.mark.parametrize("n_services", [67, 68, 90, 500, 1024, 1025])
+@pytest.mark.parametrize("mode", ["auto", "hash"])
+def test_table_modes_vs_cpp(n_services, mode, monkeypatch):
+    """Dense LDS cells (S <= 67), the emit log (68 <= S <= 1024; 90: also k_tail's mapped
+    ordered output) and the LDS hash with HBM spill (S > 1024, or forced by ZDL_TM=hash)
+    count the same links."""
+    import random
+    from tests.stress import random_trace
+    from zipkin_amd.columnar import Dictionary, pack_traces
+    if mode == "hash":
+        monkeypatch.setenv("ZDL_TM", "hash")
+    r = random.Random(n_services)
+    traces = [random_trace(r, n=r.randint(1, 30), allow_npe=False)
+              for _ in range(3000)]
+    svc, ip4, ip6 = Dictionary(), Dictionary(), Dictionary()
+    cols = pack_traces(traces, svc, ip4, ip6)
+    # spread the ids over the whole table: every partition of the log gets entries
+    perm = np.random.default_rng(n_services).permutation(n_services)[:len(svc)].astype(np.int32)
+    for f in ("local_svc", "remote_svc"):
+        a = getattr(cols, f)
+        setattr(cols, f, np.where(a >= 0, perm[np.maximum(a, 0)], -1).astype(np.int32))
+    rank = np.empty(n_services, np.int32)
+    rank[:] = np.arange(n_services) + len(svc)
+    rank[perm] = svc.ranks()
+    ctx = N.Context(n_services)
+    ctx.set_ranks(N.ZDL_DICT_SERVICE, rank)
+    ctx.set_ranks(N.ZDL_DICT_IPV4, ip4.ranks())
+    ctx.set_ranks(N.ZDL_DICT_IPV6, ip6.ranks())
+    ctx.put_spans(cols)
+    got = sorted(_tuples(*ctx.link()))
+    ctx.close()
+    st, p, c, n, e = ref.link(cols, rank, ip4.ranks(), ip6.ranks(), threads=8)
+    assert st == 0
+    assert got == sorted(_tuples(p, c, n, e))
+
+
+def test_c3_window_vs_cpp():
+    """The time window (QueryRequest.test) on the LOG-mode path."""
+    w = synth.C3.scaled(300_000)
+    cols = synth.generate(w)
+    base_ms = w.base_ts_us // 1000
+    window = (base_ms + 200_000, 100_000)
+    ctx = N.Context(w.total_services)
+    ctx.set_window(*window)
+    ctx.put_spans(cols)
+    got = sorted(_tuples(*ctx.link()))
+    ctx.close()
+    st, p, c, n, e = ref.link(cols, window=window, threads=16)
+    assert st == 0 and len(p) > 1000
+    assert got == sorted(_tuples(p, c, n, e))
+
+
+def test_c3_repeated_puts_accumulate():
+    """Several puts into one LOG-mode context add up (and reset clears)."""
+    w = synth.C3.scaled(200_000)
+    cols = synth.generate(w)
+    ctx = N.Context(w.total_services)
+    ctx.put_spans(cols)
+    one = sorted(_tuples(*ctx.link()))
+    ctx.put_spans(cols)
+    ctx.put_spans(cols)
+    three = sorted(_tuples(*ctx.link()))
+    assert [(a, b, 3 * x, 3 * y) for a, b, x, y in one] == three
+    ctx.reset()
+    assert len(ctx.link()[0]) == 0
+    ctx.close()
+    assert one == sorted(_oracle(cols))

@@ -51,6 +51,23 @@ def main():
     stats = os.path.join(g, f"prof_{a.tag}", "run_kernel_stats.csv")
     if os.path.exists(stats):
         shutil.copy(stats, os.path.join(p, f"{a.tag}_kernel_stats.csv"))
+    stats3 = os.path.join(g, f"prof_c3_{a.tag}", "run_kernel_stats.csv")
+    if os.path.exists(stats3):
+        shutil.copy(stats3, os.path.join(p, f"{a.tag}_c3_kernel_stats.csv"))
+    calib = os.path.join(g, f"calib_{a.tag}", "run_counter_collection.csv")
+    if os.path.exists(calib):  # tools/calib_fetch: 1 GiB streamed once per load width
+        cal = {}
+        for r in csv.DictReader(open(calib)):
+            n = r["Kernel_Name"]
+            if "k_stream" in n:
+                w = {"unsigned int": "4B", "unsigned long": "8B"}.get(n.split("<")[1].split(">")[0], "16B")
+                cal[w + "_per_lane"] = {"bytes_read": 1 << 30, "fetch_size_bytes": float(r["Counter_Value"]) * 1024,
+                                        "factor": (1 << 30) / (float(r["Counter_Value"]) * 1024)}
+        json.dump(cal, open(os.path.join(p, f"{a.tag}_fetch_calibration.json"), "w"), indent=1)
+    for f in ("gpu_tests", "smoke", "bench", "bench_c3"):
+        src = os.path.join(g, f"{f}_{a.tag}.log")
+        if os.path.exists(src):
+            shutil.copy(src, os.path.join(p, f"{a.tag}_{f}.log"))
     counters = {}
     for sub in os.listdir(g):
         if sub.startswith("pmc_") and sub.endswith(a.tag) and os.path.isdir(os.path.join(g, sub)):
@@ -66,7 +83,8 @@ def main():
             out = {"kernel": kern[0], "workload": a.workload, "n_spans": a.n_spans, "tag": a.tag,
                    "fetch_size_bytes_raw": fetch, "write_size_bytes": write,
                    "hbm_bytes_per_launch": 2 * fetch + write,
-                   "note": "2 x FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE correction, MI355X_MICROARCH.md §HBM)"}
+                   "note": "2 x FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE correction, MI355X_MICROARCH.md §HBM; "
+                           "the factor 2 holds for k_link's 4 and 8 B/lane loads too: profiles/*_fetch_calibration.json)"}
             json.dump(out, open(os.path.join(p, f"pmc_{a.kernel}.json"), "w"), indent=1)
             print(json.dumps(out))
     print(f"wrote profiles/{a.tag}_*")

@@ -34,9 +34,24 @@ constexpr int HCAP = 2048;          // LDS hash slots of the (parent, child) tab
 constexpr int HPROBE = 4;   // LDS hash probes before an add goes straight to HBM
 constexpr int WSMALL = 64;          // traces up to this many spans are k_link's
 constexpr int TAIL_WG = 1024;       // threads per k_tail workgroup (= BIG_WG)
-constexpr int WDENSE_MAX = 2560;    // S*S <= this -> dense u64 LDS cells (call | err << 32)
-constexpr int WTABLE_BYTES = 24576; // max(8 * (WDENSE_MAX + 64 dummy cells), 12 * HCAP)
+constexpr int WDENSE_MAX = 4544;    // S*S <= this -> dense u64 LDS cells (call | err << 32): S <= 67
+constexpr int WTABLE_BYTES = 36864; // max(8 * (WDENSE_MAX + 64 dummy cells), 12 * HCAP); two k_link
+                                    // workgroups (table + 16 wave carves) fill a CU's 160 KB
 static_assert(8 * (WDENSE_MAX + 64) <= WTABLE_BYTES && 12 * HCAP <= WTABLE_BYTES, "LDS table carve");
+// k_link with a time window carries 512 B more per wave (per-trace minima): its table stays at
+// the round-1 size so that the workgroups still share a CU
+constexpr int WDENSE_MAX_WINDOW = 2560;
+constexpr int WTABLE_BYTES_WINDOW = 24576;
+static_assert(8 * (WDENSE_MAX_WINDOW + 64) <= WTABLE_BYTES_WINDOW && 12 * HCAP <= WTABLE_BYTES_WINDOW, "LDS table carve");
+constexpr int wdense_max(int window) { return window ? WDENSE_MAX_WINDOW : WDENSE_MAX; }
+constexpr int wtable_bytes(int window) { return window ? WTABLE_BYTES_WINDOW : WTABLE_BYTES; }
+// LOG mode (WDENSE_MAX < S*S <= PMAX << PSHIFT, e.g. C3's 500 services): k_link appends every
+// link to a per-wave log in HBM and counts it per partition of 2^PSHIFT cells; k_pscan /
+// k_scatter group the log by partition, k_hist counts each partition in a dense LDS table.
+constexpr int PSHIFT = 12;          // cells per partition: 4096 u64 LDS cells = 32 KB in k_hist
+constexpr int PMAX = 256;           // partitions (per-wave LDS counters in k_link): S <= 1024
+// k_link's table modes (template parameter DENSE): hash, dense, log
+constexpr int TM_HASH = 0, TM_DENSE = 1, TM_LOG = 2;
 
 struct Cols {
   const uint64_t* id;
@@ -105,10 +120,19 @@ struct Args {
   uint32_t* o_fa;
   uint32_t* o_fb;
   uint32_t* o_bfs;
+  // LOG mode: wave gw's log segment starts at lg + lg_start[gw] (= 2 * its first span) and
+  // holds lg_n[gw] entries (cell << 1 | error); lg_cnt[p * lg_W + gw] = its entries in
+  // partition p (cell >> PSHIFT); lg_P partitions, lg_W = k_link's waves
+  uint32_t* lg;
+  uint64_t* lg_start;
+  uint32_t* lg_n;
+  uint32_t* lg_cnt;
+  uint32_t lg_P, lg_W;
 };
 
 #include "zdl_full.inc"  // the full per-window emulation (k_tail's first part)
 #include "zdl_link.inc"  // k_link, full_windows (need zdl_full.inc's helpers)
+#include "zdl_log.inc"   // LOG mode reduce: k_pscan, k_scatter, k_hist
 
 // ---------------------------------------------------------- big traces (k_tail)
 // k_tail's second part: one workgroup per trace longer than WSMALL; arrays live in HBM
@@ -675,6 +699,10 @@ struct zdl_ctx {
   DevBuf<uint32_t> big_list, counters;  // counters: big[2], cx[2], alternating by put
   uint32_t epoch = 0;
   DevBuf<uint64_t> cx_win;
+  // LOG mode (zdl_log.inc): the emit log, its grouped copy, per-wave segments and counts
+  DevBuf<uint32_t> lg, lg_grp, lg_n, lg_cnt, lg_tot;
+  DevBuf<uint64_t> lg_start;
+  int force_tm = -1;  // ZDL_TM=hash|dense|log (tests / ablation): k_link's table mode when it fits
   DevBuf<unsigned long long> prof;
   int prof_on = 0;
   DevBuf<uint64_t> b_id, b_pid;
@@ -843,20 +871,20 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
     c->cus = std::max(1, cus);
     c->grid = c->cus;  // k_tail: one 1024-thread workgroup per CU
   }
+  for (int w = 0; w < 2 && e == hipSuccess; ++w) {
+    for (int tm = 0; tm < 3 && e == hipSuccess; ++tm)
+      e = hipFuncSetAttribute(k_link_fn(tm, w), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)link_block_bytes(w, tm));
+    for (int m = 1; m <= 3 && e == hipSuccess; ++m)
+      for (int tm = 0; tm < 2 && e == hipSuccess; ++tm)
+        e = hipFuncSetAttribute(k_link_fn(tm, w, m), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)link_block_bytes(m == 3 ? 0 : w, tm));
+  }
   for (int d = 0; d < 2 && e == hipSuccess; ++d)
-    for (int w = 0; w < 2 && e == hipSuccess; ++w) {
-      e = hipFuncSetAttribute(k_link_fn(d, w), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)link_block_bytes(w));
-      for (int m = 1; m <= 2 && e == hipSuccess && d && !w; ++m)
-        e = hipFuncSetAttribute(k_link_fn(1, 0, m), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)link_block_bytes(0));
-      if (e == hipSuccess)
-        e = hipFuncSetAttribute(k_link_fn(d, w, 3), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)link_block_bytes(w));
+    for (int w = 0; w < 3 && e == hipSuccess; ++w)
       for (int o = 0; o < 2 && e == hipSuccess; ++o)
         e = hipFuncSetAttribute(k_tail_fn(d, w, o), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)tail_block_bytes(w));
-    }
   if (e == hipSuccess) {
     const char* pe = getenv("ZDL_PROF");
     c->prof_on = pe && pe[0] == '1';
@@ -866,6 +894,8 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
     }
     const char* sk = getenv("ZDL_SKIP");
     c->skip = sk ? (uint32_t)strtoul(sk, nullptr, 0) : 0u;
+    const char* ft = getenv("ZDL_TM");
+    if (ft) c->force_tm = !strcmp(ft, "hash") ? TM_HASH : (!strcmp(ft, "log") ? TM_LOG : -1);
   }
   // the initial memsets run on the context's (non-blocking) stream and are waited for
   // here: a null-stream hipMemset is not ordered before the first put's kernels on a
@@ -899,6 +929,8 @@ void zdl_destroy(zdl_ctx* c) {
     }
   }
   c->prof.release();
+  c->lg.release(); c->lg_grp.release(); c->lg_n.release(); c->lg_cnt.release(); c->lg_tot.release();
+  c->lg_start.release();
   c->b_id.release(); c->b_pid.release(); c->b_lsvc.release(); c->b_rsvc.release(); c->b_ip4.release();
   c->b_ip6.release(); c->b_parent.release(); c->b_pf.release(); c->b_perm.release(); c->b_live.release();
   c->b_hasc.release();
@@ -1006,6 +1038,9 @@ static hipError_t ensure_map(zdl_ctx* c) {
   return e;
 }
 
+// Insertion order and daily buckets: k_link only plans (mode 3), k_tail counts every window.
+static bool plan_only_mode(const zdl_ctx* c) { return c->ord || c->days; }
+
 // Default pipeline: k_link streams every trace of <= WSMALL spans; k_tail re-runs the
 // windows it queued, takes the traces it listed as longer than WSMALL and (small tables)
 // compacts the table into the mapped buffer zdl_link reads.
@@ -1013,7 +1048,14 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
                           uint64_t n_traces, const uint64_t* n_traces_dev = nullptr) {
   if (c->poisoned) return fail(c, ZDL_EDEVICE, "an earlier put failed between its kernels: call zdl_reset");
   const size_t SS = (size_t)c->rows * c->S;  // table cells (days * S * S with daily buckets)
-  const int dense = SS <= (size_t)WDENSE_MAX;
+  const int dense = SS <= (size_t)wdense_max(plan_only_mode(c) ? 0 : c->window);
+  // k_link's table mode: dense LDS cells; else the emit log when the partitions fit (S <= 1024,
+  // n_spans < 2^31: u32 positions); else the LDS hash with HBM spill
+  int tm = dense ? TM_DENSE : (SS <= ((size_t)PMAX << PSHIFT) && n_spans < (1ull << 31) ? TM_LOG : TM_HASH);
+  if (c->force_tm == TM_HASH && !dense) tm = TM_HASH;
+  if (c->force_tm == TM_LOG && SS <= ((size_t)PMAX << PSHIFT) && n_spans < (1ull << 31)) tm = TM_LOG;
+  const bool plan_only = plan_only_mode(c);  // k_link mode 3: k_tail counts every window
+  if (plan_only) tm = dense ? TM_DENSE : TM_HASH;
   const int grid = c->grid, lgrid = c->cus * lk::wgs_per_cu;  // k_link: two 16-wave workgroups per CU
   HIP_TRY(c, c->big_list.ensure(n_traces));
   // queued windows: at most one per trace; mode 3 (insertion order) uses one slot per trace
@@ -1050,6 +1092,22 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   A.cx_win = c->cx_win.p;
   A.skip = c->skip;
   A.prof = c->prof.p;
+  const uint32_t lW = (uint32_t)lgrid * (uint32_t)lk::waves(c->window);
+  const uint32_t lP = (uint32_t)((SS + (1u << PSHIFT) - 1) >> PSHIFT);
+  if (tm == TM_LOG) {
+    HIP_TRY(c, c->lg.ensure(2 * n_spans));
+    HIP_TRY(c, c->lg_grp.ensure(2 * n_spans));
+    HIP_TRY(c, c->lg_start.ensure(lW));
+    HIP_TRY(c, c->lg_n.ensure(lW));
+    HIP_TRY(c, c->lg_cnt.ensure((size_t)lP * lW));
+    HIP_TRY(c, c->lg_tot.ensure(lP));
+    A.lg = c->lg.p;
+    A.lg_start = c->lg_start.p;
+    A.lg_n = c->lg_n.p;
+    A.lg_cnt = c->lg_cnt.p;
+    A.lg_P = lP;
+    A.lg_W = lW;
+  }
   // Every buffer of the put is allocated before its first kernel is launched: a failed
   // allocation then leaves the tables, the counter slots and the epoch untouched.
   HIP_TRY(c, c->b_id.ensure(n_spans));
@@ -1099,9 +1157,21 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   ev_record(c, 1);
   const int lmode = (c->ord || c->days) ? 3 : (c->prof_on ? 1 : (c->skip ? 2 : 0));
   // A failed launch poisons nothing yet either: no kernel of this put ran
-  HIP_TRY(c, hipLaunchKernel(k_link_fn(dense, c->window, lmode), dim3(lgrid),
-                             dim3(lk::waves(c->window) * 64), kargs, link_block_bytes(c->window), c->stream));
+  HIP_TRY(c, hipLaunchKernel(k_link_fn(tm, c->window, lmode), dim3(lgrid), dim3(lk::waves(c->window) * 64), kargs,
+                             link_block_bytes(lmode == 3 ? 0 : c->window, tm), c->stream));
   ev_record(c, 7);
+  if (tm == TM_LOG) {  // group the log by partition, count each partition in LDS (zdl_log.inc)
+    hipLaunchKernelGGL(k_pscan, dim3(lP), dim3(PSCAN_WG), 0, c->stream, c->lg_cnt.p, lW, c->lg_tot.p);
+    hipLaunchKernelGGL(k_scatter, dim3(lW), dim3(SCATTER_WG), 0, c->stream, c->lg.p, c->lg_start.p, c->lg_n.p,
+                       c->lg_cnt.p, lW, lP, c->lg_tot.p, c->lg_grp.p);
+    hipLaunchKernelGGL(k_hist, dim3((unsigned)c->cus * 4), dim3(HIST_WG), 0, c->stream, c->lg_grp.p, c->lg_tot.p, lP,
+                       (uint64_t)SS, c->call.p, c->errc.p);
+    const hipError_t ke = hipGetLastError();
+    if (ke != hipSuccess) {
+      c->poisoned = true;
+      return hip_fail(c, ke, "LOG mode reduce launch");
+    }
+  }
   ev_record(c, 2);
   ev_record(c, 3);
   c->map_fresh = false;  // k_link has changed the table
