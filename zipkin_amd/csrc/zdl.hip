@@ -121,7 +121,7 @@ struct Args {
   uint32_t* o_fb;
   uint32_t* o_bfs;
   // LOG mode: wave gw's log segment starts at lg + lg_start[gw] (= 2 * its first span) and
-  // holds lg_n[gw] entries (cell << 1 | error); lg_cnt[p * lg_W + gw] = its entries in
+  // holds lg_n[gw] entries (cell << 1 | error); lg_cnt[gw * lg_P + p] = its entries in
   // partition p (cell >> PSHIFT); lg_P partitions, lg_W = k_link's waves
   uint32_t* lg;
   uint64_t* lg_start;
@@ -1100,7 +1100,7 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
     HIP_TRY(c, c->lg_start.ensure(lW));
     HIP_TRY(c, c->lg_n.ensure(lW));
     HIP_TRY(c, c->lg_cnt.ensure((size_t)lP * lW));
-    HIP_TRY(c, c->lg_tot.ensure(lP));
+    HIP_TRY(c, c->lg_tot.ensure(2 * PMAX + 1));  // totals, then the bases
     A.lg = c->lg.p;
     A.lg_start = c->lg_start.p;
     A.lg_n = c->lg_n.p;
@@ -1161,11 +1161,13 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
                              link_block_bytes(lmode == 3 ? 0 : c->window, tm), c->stream));
   ev_record(c, 7);
   if (tm == TM_LOG) {  // group the log by partition, count each partition in LDS (zdl_log.inc)
-    hipLaunchKernelGGL(k_pscan, dim3(lP), dim3(PSCAN_WG), 0, c->stream, c->lg_cnt.p, lW, c->lg_tot.p);
-    hipLaunchKernelGGL(k_scatter, dim3(lW), dim3(SCATTER_WG), 0, c->stream, c->lg.p, c->lg_start.p, c->lg_n.p,
-                       c->lg_cnt.p, lW, lP, c->lg_tot.p, c->lg_grp.p);
-    hipLaunchKernelGGL(k_hist, dim3((unsigned)c->cus * 4), dim3(HIST_WG), 0, c->stream, c->lg_grp.p, c->lg_tot.p, lP,
-                       (uint64_t)SS, c->call.p, c->errc.p);
+    hipLaunchKernelGGL(k_pscan, dim3(lP), dim3(PSCAN_WG), 0, c->stream, c->lg_cnt.p, lW, lP, c->lg_tot.p);
+    hipLaunchKernelGGL(k_pbase, dim3(1), dim3(PMAX), 0, c->stream, c->lg_tot.p, lP, c->lg_tot.p + PMAX);
+    hipLaunchKernelGGL(k_scatter, dim3((unsigned)std::min<uint32_t>(lW, (uint32_t)c->cus * 8)), dim3(SCATTER_WG), 0,
+                       c->stream, c->lg.p, c->lg_start.p, c->lg_n.p, c->lg_cnt.p, lW, lP, c->lg_tot.p + PMAX,
+                       c->lg_grp.p);
+    hipLaunchKernelGGL(k_hist, dim3((unsigned)c->cus * 4), dim3(HIST_WG), 0, c->stream, c->lg_grp.p,
+                       c->lg_tot.p + PMAX, lP, (uint64_t)SS, c->call.p, c->errc.p);
     const hipError_t ke = hipGetLastError();
     if (ke != hipSuccess) {
       c->poisoned = true;
