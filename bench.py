@@ -261,13 +261,25 @@ def main():
     # HIP events around k_link on every 8th put of the timed region (each event pair costs
     # the step a few microseconds)
     ctx = N.Context(S, device=local, timing=True, timing_stride=8)
-    tcall = torch.zeros(S * S, dtype=torch.int64, device=dev)
-    terr = torch.zeros(S * S, dtype=torch.int64, device=dev)
+    combine = "none"
+    if world > 1:
+        # libzdl joins one RCCL communicator (zdl_comm_init): zdl_link sums every rank's tables
+        # with ncclAllReduce over xGMI inside the library, as a JVM caller would get it
+        uid = [N.Context.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        try:
+            ctx.comm_init(uid[0], rank, world)
+            combine = "libzdl RCCL all-reduce (zdl_comm_init)"
+        except N.ZdlError as ex:  # keep the scaling run alive: the same sum through torch's RCCL
+            log(f"[rank {rank}] zdl_comm_init failed ({ex}); combining through torch.distributed")
+            combine = "torch.distributed all-reduce of exported tables"
+    tcall = torch.zeros(S * S, dtype=torch.int64, device=dev) if combine.startswith("torch") else None
+    terr = torch.zeros(S * S, dtype=torch.int64, device=dev) if combine.startswith("torch") else None
 
     def step():
         ctx.reset()
         ctx.put_spans_device(ptrs, cols.n_spans, doff.data_ptr(), cols.n_traces)
-        if world > 1:
+        if tcall is not None:
             ctx.table_export(tcall.data_ptr(), terr.data_ptr())
             ctx.sync()
             dist.all_reduce(tcall)
@@ -407,7 +419,7 @@ def main():
             "dtype": "u64",
             "data": "synthetic",
             "config": {"workload": w.name, "spans_per_gpu": cols.n_spans, "traces_per_gpu": cols.n_traces,
-                       "services": S, "parallelism": f"trace-shard x{world}" + (" + RCCL all-reduce" if world > 1 else ""),
+                       "services": S, "parallelism": f"trace-shard x{world}", "combine": combine,
                        "kernel_ms": {"k_link": tiles},
                        "step_roofline_frac": bytes_launch / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
                        "k_link_read_frac": read_launch / (tiles * 1e-3) / 1e9 / HBM_PEAK_GBS,

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define ZDL_ABI_VERSION 1
+#define ZDL_ABI_VERSION 2  /* 2: zdl_config.n_devices / device_ids, RCCL combine */
 
 /* ---- status codes ---- */
 #define ZDL_OK          0
@@ -104,10 +104,20 @@ typedef struct zdl_span_cols {
 } zdl_span_cols;
 
 typedef struct zdl_config {
-  int32_t  device;      /* HIP device ordinal */
+  int32_t  device;      /* HIP device ordinal (device_ids == NULL) */
   uint32_t n_services;  /* service dictionary size S; links are counted in an S x S table */
   uint32_t flags;       /* ZDL_FLAG_* */
   uint32_t timing_stride; /* ZDL_FLAG_TIMING: time k_link on every stride-th put (0, 1: every put) */
+  /* Device group: device_ids != NULL makes one context drive n_devices GPUs of
+   * this process. zdl_put_spans shards whole traces by splitmix64(trace_lo) % n_devices (the
+   * low 64 bits, as InMemoryStorage groups them, InMemoryStorage.java:163, 330, 465-467; the
+   * trace_lo column is then required), every device links its shard, and zdl_link sums the
+   * per-device tables on device_ids[0] with one RCCL reduce over xGMI (DependencyLinker.merge
+   * semantics, DependencyLinker.java:189-204) before compacting. Sorted output only: not with
+   * ZDL_FLAG_INSERTION_ORDER, zdl_set_days, the span store or mysql rows. n_devices = 1 with
+   * device_ids set runs the same path on one device. */
+  uint32_t n_devices;
+  const int32_t* device_ids;
 } zdl_config;
 
 /* Links owned by the context; valid until the next zdl_link/zdl_merge_links/zdl_destroy. */
@@ -207,9 +217,30 @@ int zdl_reset(zdl_ctx* ctx);
 
 /* Multi-GPU combine support: copy the S x S int64 call and error tables to/from device
  * buffers of the same device (e.g. for an RCCL all-reduce), ordered on the ctx stream.
- * zdl_table_import is refused on a ZDL_FLAG_INSERTION_ORDER context (no first-seen ranks). */
+ * zdl_table_import is refused on a ZDL_FLAG_INSERTION_ORDER context (no first-seen ranks).
+ * A device group exports the sum over its devices into buffers on device_ids[0] and imports
+ * into device_ids[0] (the other devices are reset); a rank that joined a job (zdl_comm_init)
+ * exports the sum over the ranks. */
 int zdl_table_export(zdl_ctx* ctx, void* dev_call, void* dev_err);
 int zdl_table_import(zdl_ctx* ctx, const void* dev_call, const void* dev_err);
+
+/* ---- multi-process jobs (one process per GPU, e.g. torch.distributed.run): each process
+ * makes a one-device context and joins one RCCL communicator; from then on zdl_link and
+ * zdl_table_export of every rank sum the tables of all ranks (ncclAllReduce over xGMI) and
+ * return the job's links. Rank 0 makes the id and sends its 128 bytes to the others. Not with
+ * ZDL_FLAG_INSERTION_ORDER or daily buckets. ---- */
+#define ZDL_COMM_ID_BYTES 128
+int zdl_comm_unique_id(uint8_t* out /* ZDL_COMM_ID_BYTES */);
+int zdl_comm_init(zdl_ctx* ctx, const uint8_t* id, int rank, int world);
+
+/* Device-resident, already sharded input of a device group: cols[d] / n_spans[d] /
+ * offsets[d] / n_traces[d] live on device_ids[d] (zdl_put_spans_device per device,
+ * asynchronous). On a one-device context, entry 0 only. */
+int zdl_put_spans_device_multi(zdl_ctx* ctx, const zdl_span_cols* cols, const uint64_t* n_spans,
+                               const uint64_t* const* offsets, const uint64_t* n_traces);
+int zdl_device_count(const zdl_ctx* ctx);
+/* out[i] = splitmix64(trace_lo[i]) % n_shards: the device (or rank) of a trace. Host only. */
+void zdl_shard_of(const uint64_t* trace_lo, uint64_t n, uint32_t n_shards, uint32_t* out);
 
 /* ---- daily buckets (the zipkin-dependencies job; ITDependencies.aggregateLinks,
  * zipkin/src/test/java/zipkin2/storage/ITDependencies.java:666-700) ----

@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version():
     from zipkin_amd import _native
-    assert _native.lib().zdl_abi_version() == 1
+    assert _native.lib().zdl_abi_version() == _native.ZDL_ABI_VERSION == 2
 
 
 def test_create_rejects_bad_config_without_device():
@@ -48,3 +48,27 @@ def test_product_does_not_import_oracle():
                 src = open(os.path.join(dirpath, f), encoding="utf-8").read()
                 assert "import oracle" not in src and "from oracle" not in src, f
                 assert "dl_ref" not in src and "liboracle" not in src, f
+
+
+def test_group_config_rejects_duplicate_devices_without_device():
+    """A device group is checked before any device call: RCCL takes one rank per device."""
+    from zipkin_amd import _native
+    L = _native.lib()
+    ids = (ctypes.c_int32 * 2)(0, 0)
+    cfg = _native.Config(0, 50, 0, 0, 2, ctypes.cast(ids, ctypes.POINTER(ctypes.c_int32)))
+    assert not L.zdl_create(ctypes.byref(cfg))
+    assert b"twice" in L.zdl_create_error()
+    cfg = _native.Config(0, 50, _native.ZDL_FLAG_INSERTION_ORDER, 0, 1, ctypes.cast(ids, ctypes.POINTER(ctypes.c_int32)))
+    assert not L.zdl_create(ctypes.byref(cfg))
+    assert b"INSERTION_ORDER" in L.zdl_create_error()
+
+
+def test_native_shard_of_matches_python_partition():
+    """The device group's host-side sharding (zdl_shard_of, C++) equals shard.shard_of, which
+    the multi-process bench and partition_columns use: the same trace lands on the same GPU."""
+    import numpy as np
+    from zipkin_amd import _native, shard
+    rng = np.random.default_rng(1)
+    lo = rng.integers(0, 2 ** 63, 100_000, dtype=np.int64).astype(np.uint64) * np.uint64(2) + np.uint64(1)
+    for n in (1, 2, 3, 8):
+        assert np.array_equal(_native.shard_of(lo, n).astype(np.int64), shard.shard_of(lo, n))

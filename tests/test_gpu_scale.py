@@ -196,3 +196,59 @@ def test_c3_repeated_puts_accumulate():
     assert len(ctx.link()[0]) == 0
     ctx.close()
     assert one == sorted(_oracle(cols))
+
+
+@pytest.mark.parametrize("config", ["c2", "c3"])
+def test_device_group_of_one_equals_single_context(config):
+    """The device-group path (zdl_config.device_ids: host sharding by splitmix64(trace_lo),
+    per-device contexts, ncclReduce of the tables, compaction of the sum) on the one device
+    the box has, against a plain context and the C++ restatement."""
+    w = synth.CONFIGS[config].scaled(200_000)
+    cols = synth.generate(w)
+    g = N.Context(w.total_services, device_ids=[0])
+    assert g.device_count() == 1
+    g.put_spans(cols)
+    g.put_spans(cols)  # accumulates like repeated putTrace
+    got = sorted(_tuples(*g.link()))
+    g.close()
+    exp = sorted(_oracle(cols))
+    assert got == [(a, b, 2 * n, 2 * e) for a, b, n, e in exp]
+
+
+def test_device_group_ungrouped_and_export():
+    import torch
+    w = synth.C4.scaled(100_000)
+    cols = synth.generate(w)
+    S = w.total_services
+    g = N.Context(S, device_ids=[0])
+    g.put_spans_ungrouped(cols)
+    dev = torch.device("cuda", 0)
+    tc = torch.zeros(S * S, dtype=torch.int64, device=dev)
+    te = torch.zeros(S * S, dtype=torch.int64, device=dev)
+    g.table_export(tc.data_ptr(), te.data_ptr())
+    g.sync()
+    torch.cuda.synchronize(dev)
+    got = sorted(_tuples(*g.link()))
+    g.close()
+    exp = sorted(_oracle(cols))
+    assert got == exp
+    c, e = tc.cpu().numpy(), te.cpu().numpy()
+    nz = np.nonzero(c)[0]
+    assert sorted((int(i) // S, int(i) % S, int(c[i]), int(e[i])) for i in nz) == exp
+
+
+@pytest.mark.parametrize("config", ["c2", "c3"])
+def test_comm_job_of_one_rank(config):
+    """zdl_comm_init with world 1: zdl_link goes through the ncclAllReduce path bench.py
+    uses at N > 1 (one process per GPU)."""
+    w = synth.CONFIGS[config].scaled(100_000)
+    cols = synth.generate(w)
+    ctx = N.Context(w.total_services)
+    ctx.comm_init(N.Context.comm_unique_id(), 0, 1)
+    ctx.put_spans(cols)
+    got = sorted(_tuples(*ctx.link()))
+    ctx.reset()
+    ctx.put_spans(cols)
+    again = sorted(_tuples(*ctx.link()))
+    ctx.close()
+    assert got == again == sorted(_oracle(cols))

@@ -37,7 +37,10 @@ EXPORTS = (
     "zdl_decoder_create", "zdl_decoder_destroy", "zdl_decoder_last_error", "zdl_decoder_bind",
     "zdl_decoder_dict_size", "zdl_decoder_missing", "zdl_decode_proto3", "zdl_decode_proto3_retry",
     "zdl_decoder_download", "zdl_decoder_kernel_ms", "zdl_put_mysql_rows", "zdl_rows_last_error",
+    "zdl_comm_unique_id", "zdl_comm_init", "zdl_put_spans_device_multi", "zdl_device_count", "zdl_shard_of",
 )
+ZDL_ABI_VERSION = 2
+ZDL_COMM_ID_BYTES = 128
 
 
 class SpanCols(C.Structure):
@@ -48,7 +51,7 @@ class SpanCols(C.Structure):
 
 class Config(C.Structure):
     _fields_ = [("device", C.c_int32), ("n_services", C.c_uint32), ("flags", C.c_uint32),
-                ("timing_stride", C.c_uint32)]
+                ("timing_stride", C.c_uint32), ("n_devices", C.c_uint32), ("device_ids", C.POINTER(C.c_int32))]
 
 
 class Links(C.Structure):
@@ -162,6 +165,18 @@ def lib() -> C.CDLL:
     L.zdl_put_mysql_rows.argtypes = [vp, C.POINTER(MysqlRows), u64, vp, u32]
     L.zdl_put_mysql_rows.restype = C.c_int
     L.zdl_rows_last_error.restype = C.c_char_p
+    L.zdl_comm_unique_id.argtypes = [vp]
+    L.zdl_comm_unique_id.restype = C.c_int
+    L.zdl_comm_init.argtypes = [vp, vp, C.c_int, C.c_int]
+    L.zdl_comm_init.restype = C.c_int
+    L.zdl_put_spans_device_multi.argtypes = [vp, C.POINTER(SpanCols), vp, vp, vp]
+    L.zdl_put_spans_device_multi.restype = C.c_int
+    L.zdl_device_count.argtypes = [vp]
+    L.zdl_device_count.restype = C.c_int
+    L.zdl_shard_of.argtypes = [vp, u64, u32, vp]
+    L.zdl_shard_of.restype = None
+    if L.zdl_abi_version() != ZDL_ABI_VERSION:
+        raise ImportError(f"{LIB_PATH} has ABI {L.zdl_abi_version()}, this binding {ZDL_ABI_VERSION}: rebuild")
     L.zdl_decoder_kernel_ms.restype = C.c_float
     L.zdl_decoder_kernel_ms.argtypes = [vp]
     for name in ("zdl_decoder_bind", "zdl_decoder_missing", "zdl_decode_proto3", "zdl_decode_proto3_retry",
@@ -183,17 +198,24 @@ class Context:
     """One zdl_ctx: a device-resident link-count table for S services."""
 
     def __init__(self, n_services: int, device: int = 0, timing: bool = False, timing_all: bool = False,
-                 timing_stride: int = 1, insertion_order: bool = False):
+                 timing_stride: int = 1, insertion_order: bool = False, device_ids=None):
+        """device_ids: a device group (zdl_config.device_ids): traces sharded over these GPUs,
+        the tables summed by RCCL at link()."""
         L = lib()
         flags = (ZDL_FLAG_TIMING if timing else 0) | (ZDL_FLAG_TIMING_ALL if timing_all else 0)
         flags |= ZDL_FLAG_INSERTION_ORDER if insertion_order else 0
-        cfg = Config(device, int(n_services), flags, int(timing_stride))
+        ids = None
+        if device_ids is not None:
+            ids = (C.c_int32 * len(device_ids))(*[int(d) for d in device_ids])
+        cfg = Config(device, int(n_services), flags, int(timing_stride), len(device_ids) if ids else 0,
+                     C.cast(ids, C.POINTER(C.c_int32)) if ids else None)
         h = L.zdl_create(C.byref(cfg))
         if not h:
             raise ZdlError(ZDL_EDEVICE, L.zdl_create_error().decode())
         self.h = C.c_void_p(h)
         self.n_services = int(n_services)
         self.insertion_order = bool(insertion_order)
+        self._group = device_ids is not None
         self._L = L
 
     def close(self):
@@ -224,8 +246,30 @@ class Context:
     def set_window(self, end_ts_ms: int, lookback_ms: int):
         self.check(self._L.zdl_set_window(self.h, int(end_ts_ms), int(lookback_ms)))
 
+    def comm_init(self, uid: bytes, rank: int, world: int) -> None:
+        """Joins a multi-process job (zdl_comm_init): link() then returns every rank's links."""
+        b = C.create_string_buffer(bytes(uid), ZDL_COMM_ID_BYTES)
+        self.check(self._L.zdl_comm_init(self.h, b, int(rank), int(world)))
+
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        b = C.create_string_buffer(ZDL_COMM_ID_BYTES)
+        rc = lib().zdl_comm_unique_id(b)
+        if rc != ZDL_OK:
+            raise ZdlError(rc, "zdl_comm_unique_id failed")
+        return b.raw
+
+    def device_count(self) -> int:
+        return int(self._L.zdl_device_count(self.h))
+
     def put_spans(self, cols) -> None:
         """cols: columnar.Columns (host numpy arrays)."""
+        if self.device_count() > 1 or self._group:
+            sc = SpanCols(_ptr(cols.trace_lo), _ptr(cols.id), _ptr(cols.parent_id), _ptr(cols.local_svc),
+                          _ptr(cols.remote_svc), _ptr(cols.local_ip4), _ptr(cols.local_ip6), _ptr(cols.port_flags),
+                          _ptr(cols.timestamp))
+            self.check(self._L.zdl_put_spans(self.h, C.byref(sc), cols.n_spans, _ptr(cols.offsets), cols.n_traces))
+            return
         sc = SpanCols(None, _ptr(cols.id), _ptr(cols.parent_id), _ptr(cols.local_svc), _ptr(cols.remote_svc),
                       _ptr(cols.local_ip4), _ptr(cols.local_ip6), _ptr(cols.port_flags), _ptr(cols.timestamp))
         self.check(self._L.zdl_put_spans(self.h, C.byref(sc), cols.n_spans, _ptr(cols.offsets), cols.n_traces))
@@ -437,3 +481,11 @@ class Decoder:
             self.close()
         except Exception:
             pass
+
+
+def shard_of(trace_lo: np.ndarray, n_shards: int) -> np.ndarray:
+    """zdl_shard_of: the device / rank of each trace_lo (host only, no device needed)."""
+    a = np.ascontiguousarray(trace_lo, np.uint64)
+    out = np.empty(len(a), np.uint32)
+    lib().zdl_shard_of(_ptr(a), len(a), int(n_shards), _ptr(out))
+    return out

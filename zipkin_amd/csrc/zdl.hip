@@ -14,6 +14,7 @@
 // zdl_link reads that (or compacts the non-zero cells itself: k_compact_ordered /
 // k_compact) and sorts by service rank when ranks are set.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include "zdl_group.h"
 
@@ -22,6 +23,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/zdl.h"
@@ -703,6 +705,15 @@ struct zdl_ctx {
   DevBuf<uint32_t> lg, lg_grp, lg_n, lg_cnt, lg_tot;
   DevBuf<uint64_t> lg_start;
   int force_tm = -1;  // ZDL_TM=hash|dense|log (tests / ablation): k_link's table mode when it fits
+  // Multi-GPU. A device group (zdl_config.device_ids): one context per device,
+  // traces sharded by splitmix64(trace_lo) % n, the tables summed by RCCL (ncclReduce to the
+  // first device) at zdl_link. A rank of a multi-process job (zdl_comm_init): the tables
+  // summed over the ranks (ncclAllReduce) at zdl_link / zdl_table_export.
+  std::vector<zdl_ctx*> sub;
+  std::vector<ncclComm_t> comms;
+  ncclComm_t comm = nullptr;
+  int comm_rank = 0, comm_world = 1;
+  DevBuf<unsigned long long> red_call, red_err;  // the summed tables
   DevBuf<unsigned long long> prof;
   int prof_on = 0;
   DevBuf<uint64_t> b_id, b_pid;
@@ -827,11 +838,41 @@ void put_times(zdl_ctx* c) {
 
 }  // namespace
 
+// ---- device groups (zdl_config.device_ids) ----
+// Runs f on every device's context; the first failure's message becomes the group's.
+template <class F>
+int group_each(zdl_ctx* g, F&& f) {
+  for (zdl_ctx* s : g->sub) {
+    const int rc = f(s);
+    if (rc != ZDL_OK) {
+      g->err = s->err;
+      return rc;
+    }
+  }
+  return ZDL_OK;
+}
+int group_first(zdl_ctx* g, int rc, zdl_ctx* s = nullptr) {
+  if (rc != ZDL_OK) g->err = (s ? s : g->sub[0])->err;
+  return rc;
+}
+int group_put(zdl_ctx* g, const zdl_span_cols* col, uint64_t n_spans, const uint64_t* off, uint64_t n_traces);
+int group_export(zdl_ctx* g, void* dev_call, void* dev_err);
+
+// splitmix64 finaliser (shard.py's): trace t goes to device splitmix64(trace_lo) % n
+inline uint64_t splitmix64(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
 extern "C" {
 
 int zdl_abi_version(void) { return ZDL_ABI_VERSION; }
 
 const char* zdl_create_error(void) { return g_create_error.c_str(); }
+
+static zdl_ctx* create_group(const zdl_config* cfg);
 
 zdl_ctx* zdl_create(const zdl_config* cfg) {
   g_create_error.clear();
@@ -839,6 +880,7 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
     g_create_error = "n_services must be in [1, 65535]";
     return nullptr;
   }
+  if (cfg->device_ids) return create_group(cfg);
   zdl_ctx* c = new zdl_ctx();
   c->device = cfg->device;
   c->S = cfg->n_services;
@@ -911,6 +953,16 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
 
 void zdl_destroy(zdl_ctx* c) {
   if (!c) return;
+  if (!c->sub.empty() || !c->comms.empty()) {  // a device group
+    for (auto& cm : c->comms)
+      if (cm) (void)ncclCommDestroy(cm);
+    for (auto* s : c->sub) zdl_destroy(s);
+    delete c;
+    return;
+  }
+  if (c->comm) (void)ncclCommDestroy(c->comm);
+  c->red_call.release();
+  c->red_err.release();
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (auto& r : c->rank) r.release();
@@ -958,10 +1010,14 @@ void zdl_destroy(zdl_ctx* c) {
 
 const char* zdl_last_error(const zdl_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
-void* zdl_stream(zdl_ctx* c) { return c ? (void*)c->stream : nullptr; }
+void* zdl_stream(zdl_ctx* c) {
+  if (c && !c->sub.empty()) return zdl_stream(c->sub[0]);
+  return c ? (void*)c->stream : nullptr;
+}
 
 int zdl_set_ranks(zdl_ctx* c, int dict, const int32_t* rank, uint32_t n) {
   if (!c || dict < 0 || dict > 2) return fail(c, ZDL_EINVAL, "bad dictionary");
+  if (!c->sub.empty()) return group_each(c, [&](zdl_ctx* s) { return zdl_set_ranks(s, dict, rank, n); });
   HIP_TRY(c, enter(c));
   c->host_rank[dict].assign(rank, rank + n);
   if (n == 0) {
@@ -977,6 +1033,7 @@ int zdl_set_ranks(zdl_ctx* c, int dict, const int32_t* rank, uint32_t n) {
 
 int zdl_set_days(zdl_ctx* c, int64_t day0_ms, uint32_t n_days) {
   if (!c) return ZDL_EINVAL;
+  if (!c->sub.empty() || c->comm) return fail(c, ZDL_EINVAL, "zdl_set_days: one device, one process");
   if (n_days > 255) return fail(c, ZDL_EINVAL, "zdl_set_days: at most 255 days");
   if (n_days && (day0_ms % DAY_MS) != 0) return fail(c, ZDL_EINVAL, "zdl_set_days: day0 must be a UTC midnight");
   if (n_days && c->window) return fail(c, ZDL_EINVAL, "zdl_set_days: not with a time window");
@@ -998,6 +1055,7 @@ int zdl_set_days(zdl_ctx* c, int64_t day0_ms, uint32_t n_days) {
 
 int zdl_set_window(zdl_ctx* c, int64_t end_ts_ms, int64_t lookback_ms) {
   if (!c) return ZDL_EINVAL;
+  if (!c->sub.empty()) return group_each(c, [&](zdl_ctx* s) { return zdl_set_window(s, end_ts_ms, lookback_ms); });
   if (c->days && lookback_ms > 0) return fail(c, ZDL_EINVAL, "zdl_set_window: not with daily buckets");
   if (lookback_ms <= 0) {
     c->window = 0;
@@ -1340,6 +1398,7 @@ int zdl_store_append(zdl_store* st, const zdl_span_cols* col, uint64_t n) {
 int zdl_put_stored(zdl_ctx* c, const zdl_store* st, const uint32_t* perm, uint64_t n_sel, const uint64_t* off,
                    uint64_t n_traces) {
   if (!c || !st || (n_sel && !perm) || !off) return fail(c, ZDL_EINVAL, "null argument");
+  if (!c->sub.empty()) return fail(c, ZDL_EINVAL, "zdl_put_stored: a store lives on one device");
   if (st->device != c->device) return fail(c, ZDL_EINVAL, "zdl_put_stored: store and context on different devices");
   if (n_traces == 0 || n_sel == 0) return ZDL_OK;
   if (off[0] != 0 || off[n_traces] != n_sel) return fail(c, ZDL_EINVAL, "trace offsets must span [0, n_sel]");
@@ -1386,6 +1445,8 @@ int zdl_put_stored(zdl_ctx* c, const zdl_store* st, const uint32_t* perm, uint64
 int zdl_put_spans_device(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans, const uint64_t* off,
                          uint64_t n_traces) {
   if (!c || !col) return fail(c, ZDL_EINVAL, "null argument");
+  if (!c->sub.empty())
+    return fail(c, ZDL_EINVAL, "zdl_put_spans_device: a device group takes zdl_put_spans or zdl_put_spans_device_multi");
   if (n_spans == 0 || (off && n_traces == 0)) return ZDL_OK;
   if (!col->id || !col->parent_id || !col->local_svc || !col->remote_svc || !col->local_ip4 ||
       !col->local_ip6 || !col->port_flags)
@@ -1400,6 +1461,7 @@ int zdl_put_spans_device(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans,
 
 int zdl_sync(zdl_ctx* c) {
   if (!c) return ZDL_EINVAL;
+  if (!c->sub.empty()) return group_each(c, [&](zdl_ctx* s) { return zdl_sync(s); });
   HIP_TRY(c, enter(c));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   uint32_t st = 0;
@@ -1411,6 +1473,7 @@ int zdl_sync(zdl_ctx* c) {
 int zdl_put_spans(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans, const uint64_t* off,
                   uint64_t n_traces) {
   if (!c || !col) return fail(c, ZDL_EINVAL, "null argument");
+  if (!c->sub.empty()) return group_put(c, col, n_spans, off, n_traces);
   if (off) {
     if (n_traces == 0) return ZDL_OK;
     if (off[0] != 0 || off[n_traces] != n_spans) return fail(c, ZDL_EINVAL, "trace offsets must span [0, n_spans]");
@@ -1470,6 +1533,7 @@ int zdl_put_spans(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans, const 
 
 int zdl_reset(zdl_ctx* c) {
   if (!c) return ZDL_EINVAL;
+  if (!c->sub.empty()) return group_each(c, [&](zdl_ctx* s) { return zdl_reset(s); });
   HIP_TRY(c, enter(c));
   if (c->poisoned) {  // the counter slots may hold a half-finished put's counts
     HIP_TRY(c, hipMemsetAsync(c->counters.p, 0, 20, c->stream));
@@ -1558,17 +1622,13 @@ static int link_insertion(zdl_ctx* c, zdl_links* out) {
   return ZDL_OK;
 }
 
-int zdl_link(zdl_ctx* c, int order, zdl_links* out) {
-  if (!c || !out) return ZDL_EINVAL;
-  if (c->days) return fail(c, ZDL_EINVAL, "daily buckets are set: use zdl_link_days");
-  if (c->poisoned) return fail(c, ZDL_EDEVICE, "an earlier put failed between its kernels: call zdl_reset");
-  if (order == ZDL_ORDER_INSERTION) {
-    if (!c->ord) return fail(c, ZDL_EINVAL, "ZDL_ORDER_INSERTION needs a ZDL_FLAG_INSERTION_ORDER context");
-    HIP_TRY(c, enter(c));
-    return link_insertion(c, out);
-  }
-  if (order != ZDL_ORDER_SORTED) return fail(c, ZDL_EINVAL, "zdl_link: order must be ZDL_ORDER_SORTED or ZDL_ORDER_INSERTION");
-  HIP_TRY(c, enter(c));
+}  // extern "C"
+
+// zdl_link's sorted output from the S x S tables (call, err) on c's device: c's own tables
+// (own: k_tail may already have compacted them into the mapped buffer) or summed ones (a
+// device group's or a multi-process job's reduction).
+static int link_sorted(zdl_ctx* c, const unsigned long long* call, const unsigned long long* err, bool own,
+                       zdl_links* out) {
   const uint64_t SS = (uint64_t)c->S * c->S;
   const bool ordered = SS <= (uint64_t)COMPACT_WG * 8;
   ev_record(c, 5);
@@ -1578,12 +1638,12 @@ int zdl_link(zdl_ctx* c, int order, zdl_links* out) {
     // status, count and records land in mapped pinned memory: written by the last put's
     // k_tail, or here when the table changed since
     HIP_TRY(c, ensure_map(c));
-    const bool tail_compacted = c->map_fresh;
-    if (!c->map_fresh) {
-      hipLaunchKernelGGL(k_compact_ordered, dim3(1), dim3(COMPACT_WG), 0, c->stream, c->call.p, c->errc.p,
-                         (uint32_t)SS, c->S, c->status.p, c->d_map);
+    const bool tail_compacted = own && c->map_fresh;
+    if (!tail_compacted) {
+      hipLaunchKernelGGL(k_compact_ordered, dim3(1), dim3(COMPACT_WG), 0, c->stream, call, err, (uint32_t)SS, c->S,
+                         c->status.p, c->d_map);
       HIP_TRY(c, hipGetLastError());
-      c->map_fresh = true;
+      c->map_fresh = own;  // h_map now holds the compaction of c's own table, or of a sum
     }
     ev_record(c, 6);
     // the last put's k_tail compacted: spin on its flag in mapped memory (a blocking
@@ -1618,8 +1678,8 @@ int zdl_link(zdl_ctx* c, int order, zdl_links* out) {
     HIP_TRY(c, c->o_call.ensure(SS));
     HIP_TRY(c, c->o_err.ensure(SS));
     uint64_t m = 0;
-    HIP_TRY(c, compact_links(c->lw, c->call.p, c->errc.p, SS, c->S, c->nrank[0] ? c->rank[0].p : nullptr,
-                             c->nrank[0], c->o_p.p, c->o_c.p, c->o_call.p, c->o_err.p, &m, c->stream));
+    HIP_TRY(c, compact_links(c->lw, call, err, SS, c->S, c->nrank[0] ? c->rank[0].p : nullptr, c->nrank[0], c->o_p.p,
+                             c->o_c.p, c->o_call.p, c->o_err.p, &m, c->stream));
     ev_record(c, 6);
     c->out_p.resize(m);
     c->out_c.resize(m);
@@ -1649,10 +1709,36 @@ int zdl_link(zdl_ctx* c, int order, zdl_links* out) {
   return ZDL_OK;
 }
 
+static int comm_sum_tables(zdl_ctx* c);  // multi-process job: every rank's tables summed (below)
+static int group_link(zdl_ctx* g, int order, zdl_links* out);
+
+extern "C" {
+
+int zdl_link(zdl_ctx* c, int order, zdl_links* out) {
+  if (!c || !out) return ZDL_EINVAL;
+  if (!c->sub.empty()) return group_link(c, order, out);
+  if (c->days) return fail(c, ZDL_EINVAL, "daily buckets are set: use zdl_link_days");
+  if (c->poisoned) return fail(c, ZDL_EDEVICE, "an earlier put failed between its kernels: call zdl_reset");
+  if (order == ZDL_ORDER_INSERTION) {
+    if (!c->ord) return fail(c, ZDL_EINVAL, "ZDL_ORDER_INSERTION needs a ZDL_FLAG_INSERTION_ORDER context");
+    HIP_TRY(c, enter(c));
+    return link_insertion(c, out);
+  }
+  if (order != ZDL_ORDER_SORTED) return fail(c, ZDL_EINVAL, "zdl_link: order must be ZDL_ORDER_SORTED or ZDL_ORDER_INSERTION");
+  HIP_TRY(c, enter(c));
+  if (c->comm) {  // a rank of a multi-process job: the links of every rank's tables
+    const int rc = comm_sum_tables(c);
+    if (rc != ZDL_OK) return rc;
+    return link_sorted(c, c->red_call.p, c->red_err.p, false, out);
+  }
+  return link_sorted(c, c->call.p, c->errc.p, true, out);
+}
+
 // Daily buckets: the cells as (day, parent, child, counts), ordered like
 // ITDependencies.aggregateLinks' map of per-day DependencyLinker.link() lists.
 int zdl_link_days(zdl_ctx* c, int order, zdl_day_links* out) {
   if (!c || !out) return ZDL_EINVAL;
+  if (!c->sub.empty() || c->comm) return fail(c, ZDL_EINVAL, "zdl_link_days: one device, one process");
   if (!c->days) return fail(c, ZDL_EINVAL, "zdl_link_days: no daily buckets (zdl_set_days)");
   if (order == ZDL_ORDER_INSERTION && !c->ord)
     return fail(c, ZDL_EINVAL, "ZDL_ORDER_INSERTION needs a ZDL_FLAG_INSERTION_ORDER context");
@@ -1756,6 +1842,7 @@ int zdl_link_days(zdl_ctx* c, int order, zdl_day_links* out) {
 int zdl_merge_links(zdl_ctx* c, const int32_t* parent, const int32_t* child, const int64_t* call_count,
                     const int64_t* error_count, uint64_t n, zdl_links* out) {
   if (!c || !out) return ZDL_EINVAL;
+  if (!c->sub.empty()) return group_first(c, zdl_merge_links(c->sub[0], parent, child, call_count, error_count, n, out));
   HIP_TRY(c, enter(c));
   const uint64_t SS = (uint64_t)c->S * c->S;
   HIP_TRY(c, c->m_call.ensure(SS));
@@ -1831,6 +1918,7 @@ int zdl_merge_links(zdl_ctx* c, const int32_t* parent, const int32_t* child, con
 int zdl_add_links(zdl_ctx* c, const int32_t* parent, const int32_t* child, const int64_t* call_count,
                   const int64_t* error_count, uint64_t n) {
   if (!c) return ZDL_EINVAL;
+  if (!c->sub.empty()) return group_first(c, zdl_add_links(c->sub[0], parent, child, call_count, error_count, n));
   if (c->days) return fail(c, ZDL_EINVAL, "zdl_add_links: not with daily buckets");
   if (n == 0) return ZDL_OK;
   HIP_TRY(c, enter(c));
@@ -1856,7 +1944,16 @@ int zdl_add_links(zdl_ctx* c, const int32_t* parent, const int32_t* child, const
 
 int zdl_table_export(zdl_ctx* c, void* dev_call, void* dev_err) {
   if (!c || !dev_call || !dev_err) return ZDL_EINVAL;
+  if (!c->sub.empty()) return group_export(c, dev_call, dev_err);
   HIP_TRY(c, enter(c));
+  if (c->comm) {  // every rank's tables, summed
+    const int rc = comm_sum_tables(c);
+    if (rc != ZDL_OK) return rc;
+    const size_t bytes = (size_t)c->rows * c->S * 8;
+    HIP_TRY(c, hipMemcpyAsync(dev_call, c->red_call.p, bytes, hipMemcpyDeviceToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(dev_err, c->red_err.p, bytes, hipMemcpyDeviceToDevice, c->stream));
+    return ZDL_OK;
+  }
   const size_t bytes = (size_t)c->rows * c->S * 8;
   HIP_TRY(c, hipMemcpyAsync(dev_call, c->call.p, bytes, hipMemcpyDeviceToDevice, c->stream));
   HIP_TRY(c, hipMemcpyAsync(dev_err, c->errc.p, bytes, hipMemcpyDeviceToDevice, c->stream));
@@ -1865,6 +1962,13 @@ int zdl_table_export(zdl_ctx* c, void* dev_call, void* dev_err) {
 
 int zdl_table_import(zdl_ctx* c, const void* dev_call, const void* dev_err) {
   if (!c || !dev_call || !dev_err) return ZDL_EINVAL;
+  if (!c->sub.empty()) {  // the first device holds the imported counts, the others none
+    for (size_t d = 1; d < c->sub.size(); ++d) {
+      const int rc = zdl_reset(c->sub[d]);
+      if (rc != ZDL_OK) return group_first(c, rc, c->sub[d]);
+    }
+    return group_first(c, zdl_table_import(c->sub[0], dev_call, dev_err));
+  }
   if (c->ord) return fail(c, ZDL_EINVAL, "zdl_table_import: the table carries no insertion-order ranks");
   HIP_TRY(c, enter(c));
   const size_t bytes = (size_t)c->rows * c->S * 8;
@@ -1876,6 +1980,7 @@ int zdl_table_import(zdl_ctx* c, const void* dev_call, const void* dev_err) {
 
 int zdl_get_kernel_times(zdl_ctx* c, zdl_kernel_times* out) {
   if (!c || !out) return ZDL_EINVAL;
+  if (!c->sub.empty()) return group_first(c, zdl_get_kernel_times(c->sub[0], out));
   if ((c->flags & ZDL_FLAG_TIMING) && c->lk_n) {  // mean k_link time of the last <= 64 puts
     HIP_TRY(c, enter(c));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -1893,6 +1998,225 @@ int zdl_get_kernel_times(zdl_ctx* c, zdl_kernel_times* out) {
   }
   *out = c->times;
   return ZDL_OK;
+}
+
+}  // extern "C"
+
+// ====================================================================== multi-GPU
+// traces are independent, so whole traces go to one device each by
+// splitmix64(trace_lo) % n (the LOW 64 bits: getDependencies groups by lowTraceId,
+// InMemoryStorage.java:163, 330, 465-467) and the per-device tables are summed once - the
+// additive reduce of DependencyLinker.merge (DependencyLinker.java:189-204) - by RCCL over xGMI.
+
+static zdl_ctx* create_group(const zdl_config* cfg) {
+  const uint32_t n = cfg->n_devices;
+  if (n == 0 || n > 64) {
+    g_create_error = "device group: n_devices must be in [1, 64]";
+    return nullptr;
+  }
+  for (uint32_t i = 0; i < n; ++i)
+    for (uint32_t j = i + 1; j < n; ++j)
+      if (cfg->device_ids[i] == cfg->device_ids[j]) {
+        g_create_error = "device group: a device appears twice (RCCL takes one rank per device)";
+        return nullptr;
+      }
+  if (cfg->flags & ZDL_FLAG_INSERTION_ORDER) {
+    g_create_error = "device group: ZDL_FLAG_INSERTION_ORDER needs one device (first-addLink ranks are per device)";
+    return nullptr;
+  }
+  zdl_ctx* g = new zdl_ctx();
+  g->S = cfg->n_services;
+  g->rows = cfg->n_services;
+  g->flags = cfg->flags;
+  g->device = cfg->device_ids[0];
+  for (uint32_t d = 0; d < n; ++d) {
+    zdl_config one = *cfg;
+    one.device = cfg->device_ids[d];
+    one.n_devices = 0;
+    one.device_ids = nullptr;
+    zdl_ctx* s = zdl_create(&one);
+    if (!s) {
+      const std::string e = g_create_error;
+      zdl_destroy(g);
+      g_create_error = "device " + std::to_string(cfg->device_ids[d]) + ": " + e;
+      return nullptr;
+    }
+    g->sub.push_back(s);
+  }
+  g->comms.assign(n, nullptr);
+  const ncclResult_t r = ncclCommInitAll(g->comms.data(), (int)n, cfg->device_ids);
+  if (r != ncclSuccess) {
+    g->comms.clear();
+    zdl_destroy(g);
+    g_create_error = std::string("device group: ncclCommInitAll: ") + ncclGetErrorString(r);
+    return nullptr;
+  }
+  return g;
+}
+
+namespace {
+template <class T>
+void gather(std::vector<T>& dst, const T* src, const std::vector<uint64_t>& idx) {
+  dst.resize(idx.size());
+  for (size_t i = 0; i < idx.size(); ++i) dst[i] = src[idx[i]];
+}
+}  // namespace
+
+int group_put(zdl_ctx* g, const zdl_span_cols* col, uint64_t n_spans, const uint64_t* off, uint64_t n_traces) {
+  if (!col->trace_lo) return fail(g, ZDL_EINVAL, "device group: traces are sharded by trace_lo, which is missing");
+  if (!col->id || !col->parent_id || !col->local_svc || !col->remote_svc || !col->local_ip4 || !col->local_ip6 ||
+      !col->port_flags)
+    return fail(g, ZDL_EINVAL, "missing column");
+  if (off) {
+    if (n_traces == 0) return ZDL_OK;
+    if (off[0] != 0 || off[n_traces] != n_spans) return fail(g, ZDL_EINVAL, "trace offsets must span [0, n_spans]");
+    for (uint64_t t = 0; t < n_traces; ++t)
+      if (off[t + 1] < off[t]) return fail(g, ZDL_EINVAL, "trace offsets are not non-decreasing");
+  }
+  if (n_spans == 0) return ZDL_OK;
+  const uint32_t N = (uint32_t)g->sub.size();
+  std::vector<std::vector<uint64_t>> idx(N), toff(N);
+  for (auto& o : toff) o.push_back(0);
+  if (off) {  // whole traces, in put order: the shard of the trace's first span's trace_lo
+    for (uint64_t t = 0; t < n_traces; ++t) {
+      const uint64_t b = off[t], e = off[t + 1];
+      if (e == b) continue;
+      const uint32_t d = (uint32_t)(splitmix64(col->trace_lo[b]) % N);
+      for (uint64_t i = b; i < e; ++i) idx[d].push_back(i);
+      toff[d].push_back(idx[d].size());
+    }
+  } else {  // ungrouped: every span by its own trace_lo, input order kept
+    for (uint64_t i = 0; i < n_spans; ++i) idx[(uint32_t)(splitmix64(col->trace_lo[i]) % N)].push_back(i);
+  }
+  std::vector<int> rc(N, ZDL_OK);
+  auto run = [&](uint32_t d) {
+    const std::vector<uint64_t>& ix = idx[d];
+    if (ix.empty()) return;
+    std::vector<uint64_t> lo, id, pid;
+    std::vector<int32_t> ls, rs, i4, i6;
+    std::vector<uint32_t> pf, ord;
+    std::vector<int64_t> ts;
+    gather(lo, col->trace_lo, ix);
+    gather(id, col->id, ix);
+    gather(pid, col->parent_id, ix);
+    gather(ls, col->local_svc, ix);
+    gather(rs, col->remote_svc, ix);
+    gather(i4, col->local_ip4, ix);
+    gather(i6, col->local_ip6, ix);
+    gather(pf, col->port_flags, ix);
+    if (col->timestamp) gather(ts, col->timestamp, ix);
+    if (col->ord) gather(ord, col->ord, ix);
+    zdl_span_cols sc{lo.data(), id.data(), pid.data(), ls.data(), rs.data(), i4.data(), i6.data(), pf.data(),
+                     col->timestamp ? ts.data() : nullptr, col->ord ? ord.data() : nullptr};
+    rc[d] = zdl_put_spans(g->sub[d], &sc, ix.size(), off ? toff[d].data() : nullptr, off ? toff[d].size() - 1 : 0);
+  };
+  std::vector<std::thread> th;  // one host thread per device: gather + upload + launch overlap
+  for (uint32_t d = 0; d < N; ++d) th.emplace_back(run, d);
+  for (auto& t : th) t.join();
+  for (uint32_t d = 0; d < N; ++d)
+    if (rc[d] != ZDL_OK) return group_first(g, rc[d], g->sub[d]);
+  return ZDL_OK;
+}
+
+// The per-device tables summed onto the first device (root of the reduce), into recv.
+static int group_reduce(zdl_ctx* g, unsigned long long* rcall, unsigned long long* rerr) {
+  const size_t SS = (size_t)g->S * g->S;
+  for (zdl_ctx* s : g->sub)
+    if (s->poisoned) return fail(g, ZDL_EDEVICE, "an earlier put failed between its kernels: call zdl_reset");
+  ncclResult_t r = ncclGroupStart();
+  for (size_t d = 0; d < g->sub.size() && r == ncclSuccess; ++d) {
+    zdl_ctx* s = g->sub[d];
+    (void)hipSetDevice(s->device);
+    r = ncclReduce(s->call.p, d == 0 ? (void*)rcall : (void*)s->call.p, SS, ncclUint64, ncclSum, 0, g->comms[d],
+                   s->stream);
+    if (r == ncclSuccess)
+      r = ncclReduce(s->errc.p, d == 0 ? (void*)rerr : (void*)s->errc.p, SS, ncclUint64, ncclSum, 0, g->comms[d],
+                     s->stream);
+  }
+  const ncclResult_t r2 = ncclGroupEnd();
+  (void)hipSetDevice(g->sub[0]->device);
+  if (r != ncclSuccess || r2 != ncclSuccess)
+    return fail(g, ZDL_EDEVICE, std::string("device group: ncclReduce: ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
+  return ZDL_OK;
+}
+
+static int group_link(zdl_ctx* g, int order, zdl_links* out) {
+  if (order != ZDL_ORDER_SORTED) return fail(g, ZDL_EINVAL, "device group: zdl_link returns ZDL_ORDER_SORTED");
+  zdl_ctx* s0 = g->sub[0];
+  for (size_t d = 1; d < g->sub.size(); ++d) {  // surfaces the other devices' status (NPE, bad ids)
+    const int rc = zdl_sync(g->sub[d]);
+    if (rc != ZDL_OK) return group_first(g, rc, g->sub[d]);
+  }
+  HIP_TRY(g, enter(s0));
+  const size_t SS = (size_t)g->S * g->S;
+  HIP_TRY(g, s0->red_call.ensure(SS));
+  HIP_TRY(g, s0->red_err.ensure(SS));
+  const int rc = group_reduce(g, s0->red_call.p, s0->red_err.p);
+  if (rc != ZDL_OK) return rc;
+  return group_first(g, link_sorted(s0, s0->red_call.p, s0->red_err.p, false, out));
+}
+
+int group_export(zdl_ctx* g, void* dev_call, void* dev_err) {
+  HIP_TRY(g, enter(g->sub[0]));
+  return group_reduce(g, (unsigned long long*)dev_call, (unsigned long long*)dev_err);
+}
+
+static int comm_sum_tables(zdl_ctx* c) {
+  const size_t SS = (size_t)c->rows * c->S;
+  HIP_TRY(c, c->red_call.ensure(SS));
+  HIP_TRY(c, c->red_err.ensure(SS));
+  ncclResult_t r = ncclGroupStart();
+  if (r == ncclSuccess) r = ncclAllReduce(c->call.p, c->red_call.p, SS, ncclUint64, ncclSum, c->comm, c->stream);
+  if (r == ncclSuccess) r = ncclAllReduce(c->errc.p, c->red_err.p, SS, ncclUint64, ncclSum, c->comm, c->stream);
+  const ncclResult_t r2 = ncclGroupEnd();
+  if (r != ncclSuccess || r2 != ncclSuccess)
+    return fail(c, ZDL_EDEVICE, std::string("ncclAllReduce: ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
+  return ZDL_OK;
+}
+
+extern "C" {
+
+int zdl_comm_unique_id(uint8_t* out) {
+  if (!out) return ZDL_EINVAL;
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return ZDL_EDEVICE;
+  memcpy(out, &id, sizeof id);
+  return ZDL_OK;
+}
+
+int zdl_comm_init(zdl_ctx* c, const uint8_t* id, int rank, int world) {
+  if (!c || !id || world < 1 || rank < 0 || rank >= world) return fail(c, ZDL_EINVAL, "zdl_comm_init: bad rank / world");
+  if (!c->sub.empty()) return fail(c, ZDL_EINVAL, "zdl_comm_init: a device group has its own communicator");
+  if (c->ord || c->days) return fail(c, ZDL_EINVAL, "zdl_comm_init: insertion order and daily buckets are per process");
+  if (c->comm) return fail(c, ZDL_EINVAL, "zdl_comm_init: already joined");
+  HIP_TRY(c, enter(c));
+  ncclUniqueId u;
+  memcpy(&u, id, sizeof u);
+  const ncclResult_t r = ncclCommInitRank(&c->comm, world, u, rank);
+  if (r != ncclSuccess) {
+    c->comm = nullptr;
+    return fail(c, ZDL_EDEVICE, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+  }
+  c->comm_rank = rank;
+  c->comm_world = world;
+  return ZDL_OK;
+}
+
+int zdl_put_spans_device_multi(zdl_ctx* c, const zdl_span_cols* cols, const uint64_t* n_spans,
+                               const uint64_t* const* offsets, const uint64_t* n_traces) {
+  if (!c || !cols || !n_spans || !offsets || !n_traces) return fail(c, ZDL_EINVAL, "null argument");
+  if (c->sub.empty()) return zdl_put_spans_device(c, &cols[0], n_spans[0], offsets[0], n_traces[0]);
+  for (size_t d = 0; d < c->sub.size(); ++d) {
+    const int rc = zdl_put_spans_device(c->sub[d], &cols[d], n_spans[d], offsets[d], n_traces[d]);
+    if (rc != ZDL_OK) return group_first(c, rc, c->sub[d]);
+  }
+  return ZDL_OK;
+}
+
+int zdl_device_count(const zdl_ctx* c) { return !c ? 0 : (c->sub.empty() ? 1 : (int)c->sub.size()); }
+
+void zdl_shard_of(const uint64_t* trace_lo, uint64_t n, uint32_t n_shards, uint32_t* out) {
+  for (uint64_t i = 0; i < n; ++i) out[i] = n_shards ? (uint32_t)(splitmix64(trace_lo[i]) % n_shards) : 0u;
 }
 
 }  // extern "C"
