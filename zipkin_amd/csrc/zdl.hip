@@ -746,8 +746,11 @@ struct zdl_ctx {
   unsigned long long* h_flag = nullptr;  // mapped pinned: the last put's k_tail stores its seq
   unsigned long long* d_flag = nullptr;
   unsigned long long seq = 0;            // puts that compacted into h_map
-  ZLink* h_links = nullptr;    // pinned link records
-  size_t h_links_cap = 0;
+  // zdl_link's large-table output: mapped pinned host columns (parent, child i32; call, err
+  // i64) that k_link_records writes over PCIe directly, no staging copy
+  unsigned char* h_rec = nullptr;
+  unsigned char* d_rec = nullptr;
+  size_t h_rec_cap = 0;
   DevBuf<uint64_t> o_first;
   DevBuf<int32_t> mi_p, mi_c;
   DevBuf<int64_t> mi_call, mi_err;
@@ -997,7 +1000,7 @@ void zdl_destroy(zdl_ctx* c) {
   if (c->h_meta) (void)hipHostFree(c->h_meta);
   if (c->h_map) (void)hipHostFree(c->h_map);
   if (c->h_flag) (void)hipHostFree(c->h_flag);
-  if (c->h_links) (void)hipHostFree(c->h_links);
+  if (c->h_rec) (void)hipHostFree(c->h_rec);
   c->mi_p.release(); c->mi_c.release(); c->mi_call.release(); c->mi_err.release();
   for (auto& ev : c->ev)
     if (ev) (void)hipEventDestroy(ev);
@@ -1672,32 +1675,37 @@ static int link_sorted(zdl_ctx* c, const unsigned long long* call, const unsigne
     c->out_call.assign(m.call, m.call + n);
     c->out_err.assign(m.err, m.err + n);
   } else {
-    // non-zero cells selected and (with ranks) radix-sorted on the device, in output order
-    HIP_TRY(c, c->o_p.ensure(SS));
-    HIP_TRY(c, c->o_c.ensure(SS));
-    HIP_TRY(c, c->o_call.ensure(SS));
-    HIP_TRY(c, c->o_err.ensure(SS));
+    // non-zero cells selected and (with ranks) radix-sorted on the device, in output order,
+    // written straight into mapped pinned host columns sized by the link count
     uint64_t m = 0;
-    HIP_TRY(c, compact_links(c->lw, call, err, SS, c->S, c->nrank[0] ? c->rank[0].p : nullptr, c->nrank[0], c->o_p.p,
-                             c->o_c.p, c->o_call.p, c->o_err.p, &m, c->stream));
-    ev_record(c, 6);
-    c->out_p.resize(m);
-    c->out_c.resize(m);
-    c->out_call.resize(m);
-    c->out_err.resize(m);
-    HIP_TRY(c, hipMemcpyAsync(c->h_meta, c->status.p, 16, hipMemcpyDeviceToHost, c->stream));
-    if (m) {
-      HIP_TRY(c, hipMemcpyAsync(c->out_p.data(), c->o_p.p, m * 4, hipMemcpyDeviceToHost, c->stream));
-      HIP_TRY(c, hipMemcpyAsync(c->out_c.data(), c->o_c.p, m * 4, hipMemcpyDeviceToHost, c->stream));
-      HIP_TRY(c, hipMemcpyAsync(c->out_call.data(), c->o_call.p, m * 8, hipMemcpyDeviceToHost, c->stream));
-      HIP_TRY(c, hipMemcpyAsync(c->out_err.data(), c->o_err.p, m * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, compact_select(c->lw, call, SS, &m, c->stream));
+    if (m > c->h_rec_cap) {
+      if (c->h_rec) (void)hipHostFree(c->h_rec);
+      c->h_rec = nullptr;
+      c->d_rec = nullptr;
+      c->h_rec_cap = 0;
+      const size_t cap = std::max<size_t>((size_t)(m + m / 2 + 1) & ~(size_t)1, 1024);
+      HIP_TRY(c, hipHostMalloc((void**)&c->h_rec, cap * 24, hipHostMallocMapped | hipHostMallocCoherent));
+      HIP_TRY(c, hipHostGetDevicePointer((void**)&c->d_rec, c->h_rec, 0));
+      c->h_rec_cap = cap;
     }
+    const size_t cap = c->h_rec_cap;
+    HIP_TRY(c, compact_records(c->lw, call, err, m, c->S, c->nrank[0] ? c->rank[0].p : nullptr, c->nrank[0],
+                               (int32_t*)c->d_rec, (int32_t*)(c->d_rec + 4 * cap), (int64_t*)(c->d_rec + 8 * cap),
+                               (int64_t*)(c->d_rec + 16 * cap), c->stream));
+    ev_record(c, 6);
+    HIP_TRY(c, hipMemcpyAsync(c->h_meta, c->status.p, 16, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     put_times(c);
     c->times.compact_ms = ev_ms(c, 5, 6);
     const int rc = status_code(c, (uint32_t)c->h_meta[0]);
     if (rc != ZDL_OK) return rc;
-    n = (size_t)m;
+    out->n = m;
+    out->parent = (const int32_t*)c->h_rec;
+    out->child = (const int32_t*)(c->h_rec + 4 * cap);
+    out->call_count = (const int64_t*)(c->h_rec + 8 * cap);
+    out->error_count = (const int64_t*)(c->h_rec + 16 * cap);
+    return ZDL_OK;
   }
   // cell order is (parent id, child id) order; names order needs the service rank table
   if (ordered && c->nrank[0] != 0) sort_output(c, n);  // the large path came sorted

@@ -41,11 +41,19 @@ struct LinkWork {
   uint32_t* sel[2] = {};
   uint32_t* keys[2] = {};
   uint64_t* count = nullptr;
+  uint64_t* h_count = nullptr;  // pinned
   size_t cap = 0;
   void release();
 };
 hipError_t compact_links(LinkWork& w, const unsigned long long* call, const unsigned long long* err, uint64_t SS,
                          uint32_t S, const int32_t* rank, uint32_t nrank, int32_t* parent, int32_t* child,
                          int64_t* call_out, int64_t* err_out, uint64_t* n_out, hipStream_t s);
+// The same in two steps, so that the caller can size the output by the link count first:
+// compact_select selects the non-zero cells and returns their number (one stream sync);
+// compact_records writes the m records (the output may be mapped pinned host memory).
+hipError_t compact_select(LinkWork& w, const unsigned long long* call, uint64_t SS, uint64_t* n_out, hipStream_t s);
+hipError_t compact_records(LinkWork& w, const unsigned long long* call, const unsigned long long* err, uint64_t m,
+                           uint32_t S, const int32_t* rank, uint32_t nrank, int32_t* parent, int32_t* child,
+                           int64_t* call_out, int64_t* err_out, hipStream_t s);
 
 }  // namespace zdl

@@ -149,16 +149,16 @@ void LinkWork::release() {
   for (auto*& q : sel) { if (q) (void)hipFree(q); q = nullptr; }
   for (auto*& q : keys) { if (q) (void)hipFree(q); q = nullptr; }
   if (count) (void)hipFree(count);
+  if (h_count) (void)hipHostFree(h_count);
   if (tmp) (void)hipFree(tmp);
   count = nullptr;
+  h_count = nullptr;
   tmp = nullptr;
   tmp_bytes = 0;
   cap = 0;
 }
 
-hipError_t compact_links(LinkWork& w, const unsigned long long* call, const unsigned long long* err, uint64_t SS,
-                         uint32_t S, const int32_t* rank, uint32_t nrank, int32_t* parent, int32_t* child,
-                         int64_t* call_out, int64_t* err_out, uint64_t* n_out, hipStream_t s) {
+hipError_t compact_select(LinkWork& w, const unsigned long long* call, uint64_t SS, uint64_t* n_out, hipStream_t s) {
   if (SS == 0 || SS >= (1ull << 32)) return hipErrorInvalidValue;
   if (SS > w.cap) {
     for (int b = 0; b < 2; ++b) {
@@ -166,6 +166,7 @@ hipError_t compact_links(LinkWork& w, const unsigned long long* call, const unsi
       GTRY(grow(w.keys[b], SS));
     }
     if (!w.count) GTRY(hipMalloc((void**)&w.count, sizeof(uint64_t)));
+    if (!w.h_count) GTRY(hipHostMalloc((void**)&w.h_count, sizeof(uint64_t), hipHostMallocDefault));
     size_t a = 0, b = 0;
     GTRY(hipcub::DeviceSelect::If(nullptr, a, hipcub::CountingInputIterator<uint32_t>(0), w.sel[0], w.count, (int)SS,
                                   NonZeroCell{call}, s));
@@ -183,22 +184,34 @@ hipError_t compact_links(LinkWork& w, const unsigned long long* call, const unsi
   size_t bytes = w.tmp_bytes;
   GTRY(hipcub::DeviceSelect::If(w.tmp, bytes, hipcub::CountingInputIterator<uint32_t>(0), w.sel[0], w.count, (int)SS,
                                 NonZeroCell{call}, s));
-  uint64_t m = 0;
-  GTRY(hipMemcpyAsync(&m, w.count, 8, hipMemcpyDeviceToHost, s));
+  GTRY(hipMemcpyAsync(w.h_count, w.count, 8, hipMemcpyDeviceToHost, s));  // pinned: a DMA, no staging
   GTRY(hipStreamSynchronize(s));
-  *n_out = m;
+  *n_out = *w.h_count;
+  return hipSuccess;
+}
+
+hipError_t compact_records(LinkWork& w, const unsigned long long* call, const unsigned long long* err, uint64_t m,
+                           uint32_t S, const int32_t* rank, uint32_t nrank, int32_t* parent, int32_t* child,
+                           int64_t* call_out, int64_t* err_out, hipStream_t s) {
   if (m == 0) return hipSuccess;
   const uint32_t* sel = w.sel[0];
   if (rank) {
     hipLaunchKernelGGL(k_link_keys, blocks(m), dim3(256), 0, s, w.sel[0], w.count, S, rank, nrank, w.keys[0]);
     GTRY(hipGetLastError());
-    bytes = w.tmp_bytes;
+    size_t bytes = w.tmp_bytes;
     GTRY(hipcub::DeviceRadixSort::SortPairs(w.tmp, bytes, w.keys[0], w.keys[1], w.sel[0], w.sel[1], (int)m, 0, 32, s));
     sel = w.sel[1];
   }
   hipLaunchKernelGGL(k_link_records, blocks(m), dim3(256), 0, s, sel, w.count, S, call, err, parent, child,
                      call_out, err_out);
   return hipGetLastError();
+}
+
+hipError_t compact_links(LinkWork& w, const unsigned long long* call, const unsigned long long* err, uint64_t SS,
+                         uint32_t S, const int32_t* rank, uint32_t nrank, int32_t* parent, int32_t* child,
+                         int64_t* call_out, int64_t* err_out, uint64_t* n_out, hipStream_t s) {
+  GTRY(compact_select(w, call, SS, n_out, s));
+  return compact_records(w, call, err, *n_out, S, rank, nrank, parent, child, call_out, err_out, s);
 }
 
 }  // namespace zdl
