@@ -81,6 +81,10 @@ extern "C" {
                                         zdl_link can return ZDL_ORDER_INSERTION; puts take the exact
                                         per-trace path (slower than the default streaming path); traces
                                         are limited to 2^21 spans */
+#define ZDL_FLAG_TREE_EXPORT 8u      /* with ZDL_FLAG_INSERTION_ORDER: every put also records the tree
+                                        SpanNode.Builder builds (SpanNode.java:122-249), read back by
+                                        zdl_tree_export (parity tests of the tree itself, not only its
+                                        links) */
 
 /*
  * Span columns, structure of arrays, n_spans entries each. A local endpoint is
@@ -188,6 +192,15 @@ int         zdl_store_clear(zdl_store* store);
 uint64_t    zdl_store_size(const zdl_store* store);
 int zdl_put_stored(zdl_ctx* ctx, const zdl_store* store, const uint32_t* perm, uint64_t n_sel,
                    const uint64_t* trace_offsets, uint64_t n_traces);
+
+/* ZDL_FLAG_TREE_EXPORT: the last put's trees, per input span i (its column index in the put):
+ * node_of[i] = column index of the head fragment of the cleaned span i belongs to (Trace.merge,
+ * Trace.java:28-87: the first fragment of its merge run in sorted order); parent[i] = the
+ * parent node's head index, -1 the synthetic root (SpanNode.java:145-147), -2 i is the root,
+ * -3 i is not a tree node (an absorbed fragment or a span SpanNode.Builder leaves out);
+ * bfs[i] = the node's index in SpanNode.traverse order (SpanNode.java:64-89; the synthetic root
+ * not counted), -1 unreachable. n = the last put's span count. Synchronous. */
+int zdl_tree_export(zdl_ctx* ctx, int32_t* node_of, int32_t* parent, int32_t* bfs, uint64_t n);
 
 /* Waits for the context stream and reports device-side status (e.g. ZDL_EREF_NPE). */
 int zdl_sync(zdl_ctx* ctx);

@@ -186,10 +186,19 @@ class _SpanBuilder:
 
 def trace_merge(spans: List[Span]) -> List[Span]:
     """Trace.merge (internal/Trace.java:28-87)."""
+    return trace_merge_sources(spans)[0]
+
+
+def trace_merge_sources(spans: List[Span]):
+    """Trace.merge, also returning for every output span the input indices it was merged
+    from, in Trace.merge's sorted order (the first is the head fragment). Test helper for the
+    GPU tree export (zdl_tree_export); the merge itself is the same code path."""
     length = len(spans)
     if length <= 1:
-        return spans
-    result = sorted(spans, key=functools.cmp_to_key(cleanup_compare))
+        return spans, [[i] for i in range(length)]
+    order = sorted(range(length), key=functools.cmp_to_key(lambda a, b: cleanup_compare(spans[a], spans[b])))
+    result = [spans[k] for k in order]
+    sources = [[k] for k in order]
 
     # longest trace id wins (Trace.java:34-39)
     trace_id = spans[0].trace_id
@@ -223,6 +232,7 @@ def trace_merge(spans: List[Span]) -> List[Span]:
                 previous = nxt  # Q7: the raw fragment, not the merged value (Trace.java:69)
                 length -= 1
                 del result[i + 1]
+                sources[i].extend(sources.pop(i + 1))
                 continue
             if next_shared and nxt.parent_id is None and previous.parent_id is not None:
                 # shared RPC server span that wasn't propagated its parent (Trace.java:76-79)
@@ -231,7 +241,7 @@ def trace_merge(spans: List[Span]) -> List[Span]:
         if replacement is not None:
             result[i] = replacement.build()
         i += 1
-    return result
+    return result, sources
 
 
 # ------------------------------------------------------------------- SpanNode
@@ -283,10 +293,13 @@ class SpanNodeBuilder:
         if self.log is not None:
             self.log.append(msg)
 
-    def build(self, spans: List[Span]) -> SpanNode:
+    def build(self, spans: List[Span], cleaned: Optional[List[Span]] = None) -> SpanNode:
+        """cleaned: Trace.merge(spans) already computed (tree_heads passes it to keep the
+        merged span objects, whose identity maps nodes back to input fragments)."""
         if not spans:
             raise ReferenceIAE("spans were empty")
-        cleaned = trace_merge(spans)
+        if cleaned is None:
+            cleaned = trace_merge(spans)
         trace_id = cleaned[0].trace_id
         self._fine(f"building trace tree: traceId={trace_id}")
         for s in cleaned:
@@ -610,6 +623,29 @@ class _Desc:
 
 
 # ------------------------------------------------------------- tree debugging
+def tree_heads(spans: List[Span]):
+    """Test helper: the tree SpanNode.Builder builds for one trace, as
+    {head input index: (parent head index | -1 synthetic root | -2 the root itself, BFS index)}
+    over the nodes SpanNode.traverse visits (the synthetic root not counted). A node's head is
+    the first input fragment of its merged span in Trace.merge's sorted order."""
+    cleaned, sources = trace_merge_sources(spans)
+    head_of = {id(s): src[0] for s, src in zip(cleaned, sources)}
+    root = SpanNodeBuilder().build(spans, cleaned)
+    out, k = {}, 0
+    for n in root.traverse():
+        if n.span is None:
+            continue
+        if n.parent is None:
+            par = -2
+        elif n.parent.span is None:
+            par = -1
+        else:
+            par = head_of[id(n.parent.span)]
+        out[head_of[id(n.span)]] = (par, k)
+        k += 1
+    return out
+
+
 def tree_parents(spans: List[Span]):
     """Builds the tree like SpanNode.Builder and returns, for the tree, a list of
     (node_span, parent_span_or_None, reachable) in BFS order. Test helper."""

@@ -92,3 +92,18 @@ def test_npe_on_remote_endpoint_fragment():
     b = span2("a", None, "a", Kind.SERVER, "web", None, False)
     with pytest.raises(O.ReferenceNPE):
         O.DependencyLinker().put_trace([a, b])
+
+
+@pytest.mark.parametrize("case", [c for c in SN["cases"] if "children" in c], ids=lambda c: c["name"])
+def test_tree_heads_helper_matches_golden_children(case):
+    """oracle.tree_heads (the export the GPU tree is compared with) agrees with the
+    reference's expected tree shape: every listed child hangs under its parent, children in
+    the listed order (consecutive BFS indices), the root as listed."""
+    inputs = spans(case["spans"])
+    heads = O.tree_heads(inputs)
+    if case.get("root") is not None:
+        assert heads[case["root"]] == (-2, 0)
+    for parent_i, child_is in case["children"]:
+        want = -1 if parent_i is None else parent_i
+        got = [i for i, (p, _) in sorted(heads.items(), key=lambda kv: kv[1][1]) if p == want]
+        assert got == child_is

@@ -17,6 +17,7 @@ ZDL_ORDER_SORTED, ZDL_ORDER_FIRST_SEEN, ZDL_ORDER_INSERTION = 0, 1, 2
 ZDL_FLAG_TIMING = 1
 ZDL_FLAG_TIMING_ALL = 2
 ZDL_FLAG_INSERTION_ORDER = 4
+ZDL_FLAG_TREE_EXPORT = 8
 ZDL_AKEY_NONE, ZDL_AKEY_LC, ZDL_AKEY_CA, ZDL_AKEY_CS, ZDL_AKEY_SA, ZDL_AKEY_SR, ZDL_AKEY_ERROR = range(7)
 
 PF_KIND_SHIFT = 16
@@ -38,6 +39,7 @@ EXPORTS = (
     "zdl_decoder_dict_size", "zdl_decoder_missing", "zdl_decode_proto3", "zdl_decode_proto3_retry",
     "zdl_decoder_download", "zdl_decoder_kernel_ms", "zdl_put_mysql_rows", "zdl_rows_last_error",
     "zdl_comm_unique_id", "zdl_comm_init", "zdl_put_spans_device_multi", "zdl_device_count", "zdl_shard_of",
+    "zdl_tree_export",
 )
 ZDL_ABI_VERSION = 2
 ZDL_COMM_ID_BYTES = 128
@@ -175,6 +177,8 @@ def lib() -> C.CDLL:
     L.zdl_device_count.restype = C.c_int
     L.zdl_shard_of.argtypes = [vp, u64, u32, vp]
     L.zdl_shard_of.restype = None
+    L.zdl_tree_export.argtypes = [vp, vp, vp, vp, u64]
+    L.zdl_tree_export.restype = C.c_int
     if L.zdl_abi_version() != ZDL_ABI_VERSION:
         raise ImportError(f"{LIB_PATH} has ABI {L.zdl_abi_version()}, this binding {ZDL_ABI_VERSION}: rebuild")
     L.zdl_decoder_kernel_ms.restype = C.c_float
@@ -198,12 +202,14 @@ class Context:
     """One zdl_ctx: a device-resident link-count table for S services."""
 
     def __init__(self, n_services: int, device: int = 0, timing: bool = False, timing_all: bool = False,
-                 timing_stride: int = 1, insertion_order: bool = False, device_ids=None):
+                 timing_stride: int = 1, insertion_order: bool = False, device_ids=None,
+                 tree_export: bool = False):
         """device_ids: a device group (zdl_config.device_ids): traces sharded over these GPUs,
         the tables summed by RCCL at link()."""
         L = lib()
         flags = (ZDL_FLAG_TIMING if timing else 0) | (ZDL_FLAG_TIMING_ALL if timing_all else 0)
         flags |= ZDL_FLAG_INSERTION_ORDER if insertion_order else 0
+        flags |= ZDL_FLAG_TREE_EXPORT if tree_export else 0
         ids = None
         if device_ids is not None:
             ids = (C.c_int32 * len(device_ids))(*[int(d) for d in device_ids])
@@ -258,6 +264,12 @@ class Context:
         if rc != ZDL_OK:
             raise ZdlError(rc, "zdl_comm_unique_id failed")
         return b.raw
+
+    def tree_export(self, n_spans: int):
+        """ZDL_FLAG_TREE_EXPORT: (node_of, parent, bfs) int32 arrays of the last put (zdl.h)."""
+        out = [np.empty(n_spans, np.int32) for _ in range(3)]
+        self.check(self._L.zdl_tree_export(self.h, *(_ptr(a) for a in out), int(n_spans)))
+        return tuple(out)
 
     def device_count(self) -> int:
         return int(self._L.zdl_device_count(self.h))

@@ -130,6 +130,11 @@ struct Args {
   uint32_t* lg_n;
   uint32_t* lg_cnt;
   uint32_t lg_P, lg_W;
+  // ZDL_FLAG_TREE_EXPORT (insertion-order contexts): per span of the put, its node's head
+  // slot, its parent's head slot (-1 synthetic root, -2 root, -3 no node) and BFS index
+  int32_t* tr_node;
+  int32_t* tr_parent;
+  int32_t* tr_bfs;
 };
 
 #include "zdl_full.inc"  // the full per-window emulation (k_tail's first part)
@@ -434,6 +439,24 @@ __device__ __forceinline__ void big_traces(const Args& A) {
       big_bfs(v, n, rp, A.o_key + b, A.o_fa + b, A.o_fb + b, bfs);
       big_sync();
     }
+    if (ORD && A.tr_parent) {  // ZDL_FLAG_TREE_EXPORT (wave_tree_export's encoding)
+      for (int p = threadIdx.x; p < n; p += BIG_WG) {
+        int head = p;
+        while (!v.live[head] && head > 0 && v.id[v.perm[head - 1]] == v.id[v.perm[p]]) --head;
+        const uint64_t slot = b + v.perm[p];
+        A.tr_node[slot] = (int32_t)(b + v.perm[head]);
+        const int par = v.parent[p];
+        int32_t pr = -3, bf = -1;
+        if (v.live[p] && par != PAR_NONMEMBER) {
+          pr = p == rp ? -2 : (par == PAR_TERMINAL ? -1 : (int32_t)(b + v.perm[par]));
+          int q = par, steps = 0;
+          while (q >= 0 && steps++ <= n) q = v.parent[q];
+          if (q == PAR_TERMINAL) bf = (int32_t)bfs[p];
+        }
+        A.tr_parent[slot] = pr;
+        A.tr_bfs[slot] = bf;
+      }
+    }
     for (int p = threadIdx.x; p < n; p += BIG_WG) {
       if (v.parent[p] == PAR_NONMEMBER) continue;
       link_node(v, p, rp, n, [&](int32_t a, int32_t c, bool e, int k) {
@@ -705,6 +728,8 @@ struct zdl_ctx {
   DevBuf<uint32_t> lg, lg_grp, lg_n, lg_cnt, lg_tot;
   DevBuf<uint64_t> lg_start;
   int force_tm = -1;  // ZDL_TM=hash|dense|log (tests / ablation): k_link's table mode when it fits
+  DevBuf<int32_t> tr_node, tr_parent, tr_bfs;  // ZDL_FLAG_TREE_EXPORT: the last put's tree
+  uint64_t tr_n = 0;
   // Multi-GPU. A device group (zdl_config.device_ids): one context per device,
   // traces sharded by splitmix64(trace_lo) % n, the tables summed by RCCL (ncclReduce to the
   // first device) at zdl_link. A rank of a multi-process job (zdl_comm_init): the tables
@@ -889,6 +914,11 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
   c->S = cfg->n_services;
   c->flags = cfg->flags;
   c->ord = (cfg->flags & ZDL_FLAG_INSERTION_ORDER) != 0;
+  if ((cfg->flags & ZDL_FLAG_TREE_EXPORT) && !c->ord) {
+    delete c;
+    g_create_error = "ZDL_FLAG_TREE_EXPORT needs ZDL_FLAG_INSERTION_ORDER (the exact per-trace path)";
+    return nullptr;
+  }
   c->rows = cfg->n_services;
   c->lk_stride = std::max<uint32_t>(1u, cfg->timing_stride);
   hipError_t e = hipSetDevice(c->device);
@@ -986,6 +1016,7 @@ void zdl_destroy(zdl_ctx* c) {
   c->prof.release();
   c->lg.release(); c->lg_grp.release(); c->lg_n.release(); c->lg_cnt.release(); c->lg_tot.release();
   c->lg_start.release();
+  c->tr_node.release(); c->tr_parent.release(); c->tr_bfs.release();
   c->b_id.release(); c->b_pid.release(); c->b_lsvc.release(); c->b_rsvc.release(); c->b_ip4.release();
   c->b_ip6.release(); c->b_parent.release(); c->b_pf.release(); c->b_perm.release(); c->b_live.release();
   c->b_hasc.release();
@@ -1193,6 +1224,18 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   A.b_parent = c->b_parent.p;
   A.b_live = c->b_live.p;
   A.b_haschild = c->b_hasc.p;
+  if (c->flags & ZDL_FLAG_TREE_EXPORT) {  // the last put's tree (insertion-order contexts only)
+    HIP_TRY(c, c->tr_node.ensure(n_spans));
+    HIP_TRY(c, c->tr_parent.ensure(n_spans));
+    HIP_TRY(c, c->tr_bfs.ensure(n_spans));
+    HIP_TRY(c, hipMemsetAsync(c->tr_node.p, 0xFF, n_spans * 4, c->stream));
+    HIP_TRY(c, hipMemsetAsync(c->tr_parent.p, 0xFF, n_spans * 4, c->stream));
+    HIP_TRY(c, hipMemsetAsync(c->tr_bfs.p, 0xFF, n_spans * 4, c->stream));
+    A.tr_node = c->tr_node.p;
+    A.tr_parent = c->tr_parent.p;
+    A.tr_bfs = c->tr_bfs.p;
+    c->tr_n = n_spans;
+  }
   if (c->ord) {
     HIP_TRY(c, c->o_key.ensure(n_spans));
     HIP_TRY(c, c->o_fa.ensure(n_spans));
@@ -2225,6 +2268,23 @@ int zdl_device_count(const zdl_ctx* c) { return !c ? 0 : (c->sub.empty() ? 1 : (
 
 void zdl_shard_of(const uint64_t* trace_lo, uint64_t n, uint32_t n_shards, uint32_t* out) {
   for (uint64_t i = 0; i < n; ++i) out[i] = n_shards ? (uint32_t)(splitmix64(trace_lo[i]) % n_shards) : 0u;
+}
+
+}  // extern "C"
+
+extern "C" {
+
+int zdl_tree_export(zdl_ctx* c, int32_t* node_of, int32_t* parent, int32_t* bfs, uint64_t n) {
+  if (!c || !node_of || !parent || !bfs) return ZDL_EINVAL;
+  if (!(c->flags & ZDL_FLAG_TREE_EXPORT) || !c->sub.empty()) return fail(c, ZDL_EINVAL, "context without ZDL_FLAG_TREE_EXPORT");
+  if (n != c->tr_n) return fail(c, ZDL_EINVAL, "zdl_tree_export: n must be the last put's span count");
+  const int rc = zdl_sync(c);
+  if (rc != ZDL_OK) return rc;
+  if (n == 0) return ZDL_OK;
+  HIP_TRY(c, hipMemcpy(node_of, c->tr_node.p, n * 4, hipMemcpyDeviceToHost));
+  HIP_TRY(c, hipMemcpy(parent, c->tr_parent.p, n * 4, hipMemcpyDeviceToHost));
+  HIP_TRY(c, hipMemcpy(bfs, c->tr_bfs.p, n * 4, hipMemcpyDeviceToHost));
+  return ZDL_OK;
 }
 
 }  // extern "C"
