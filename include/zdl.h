@@ -189,6 +189,10 @@ void        zdl_store_destroy(zdl_store* store);
 const char* zdl_store_last_error(const zdl_store* store);
 int         zdl_store_append(zdl_store* store, const zdl_span_cols* cols, uint64_t n_spans);
 int         zdl_store_clear(zdl_store* store);
+/* Keeps the stored spans keep[0..n_keep) (ascending positions), in that order, and frees the
+ * rest: what InMemoryStorage's deleteOldestTrace releases (InMemoryStorage.java:193-211), in
+ * one device gather once evicted spans pile up. Positions are renumbered 0..n_keep). */
+int         zdl_store_compact(zdl_store* store, const uint32_t* keep, uint64_t n_keep);
 uint64_t    zdl_store_size(const zdl_store* store);
 int zdl_put_stored(zdl_ctx* ctx, const zdl_store* store, const uint32_t* perm, uint64_t n_sel,
                    const uint64_t* trace_offsets, uint64_t n_traces);

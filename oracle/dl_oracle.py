@@ -550,6 +550,35 @@ class InMemoryStorage:
             linker.put_trace(trace)
         return linker.link()
 
+    def get_traces_all(self) -> List[List[Span]]:
+        """getTraces() (InMemoryStorage.java:251-262): every trace unconditionally, lowTraceId
+        in TreeMap(STRING_COMPARATOR) order, split by the full trace id (strictByTraceId,
+        :241-249) when strictTraceId."""
+        result: List[List[Span]] = []
+        for low in sorted(self.trace_keys):
+            same = self.spans_by_trace_id(low)
+            if self.strict_trace_id:
+                result.extend(strict_by_trace_id(same))
+            else:
+                result.append(same)
+        return result
+
+    def get_dependencies_all(self) -> List[DependencyLink]:
+        """getDependencies() (InMemoryStorage.java:265-270, used by ZipkinRule): the links of
+        getTraces(), through LinkDependencies (:334-348)."""
+        linker = DependencyLinker()
+        for trace in self.get_traces_all():
+            linker.put_trace(trace)
+        return linker.link()
+
+
+def strict_by_trace_id(spans: List[Span]) -> List[List[Span]]:
+    """InMemoryStorage.strictByTraceId (:241-249): LinkedHashMap by the full trace id."""
+    groups: Dict[str, List[Span]] = {}
+    for s in spans:
+        groups.setdefault(s.trace_id, []).append(s)
+    return list(groups.values())
+
 
 # ------------------------------------------------- daily buckets (zipkin-dependencies)
 # zipkin/src/test/java/zipkin2/storage/ITDependencies.java:666-700,

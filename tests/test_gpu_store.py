@@ -38,9 +38,11 @@ def _batches(seed, n_batches=6):
 
 
 @pytest.mark.parametrize("seed", range(30))
-@pytest.mark.parametrize("max_spans", [500000, 60])
-def test_store_vs_oracle_ims(seed, max_spans):
-    store = InMemoryStorage(max_span_count=max_spans)
+@pytest.mark.parametrize("max_spans,compact_min", [(500000, 1 << 16), (60, 1 << 16), (60, 4)])
+def test_store_vs_oracle_ims(seed, max_spans, compact_min):
+    """compact_min 4: evicted spans are released by zdl_store_compact after nearly every
+    eviction, renumbering the store under the host index."""
+    store = InMemoryStorage(max_span_count=max_spans, compact_min=compact_min)
     ref = O.InMemoryStorage(max_span_count=max_spans)
     end_ms = (BASE_US + 10_000_000_000) // 1000 + 1000
     for b in _batches(seed):
@@ -85,3 +87,55 @@ def test_store_append_grows_and_selection_is_checked():
         ctx.put_stored(st, np.array([cols.n_spans], np.uint32), np.array([0, 1], np.uint64))
     ctx.close()
     st.close()
+
+
+def _mixed_width_batches(seed, n_batches=5):
+    """Traces whose spans carry the 128-bit id or only its low half (both normalized forms),
+    so that strictTraceId splits a low trace id into two traces."""
+    r = random.Random(seed)
+    out = []
+    for _ in range(n_batches):
+        batch = []
+        for _ in range(r.randint(1, 4)):
+            lo = format(r.getrandbits(64) | 1, "016x")
+            hi = format(r.getrandbits(64) | 1, "016x")
+            ts0 = BASE_US + r.randrange(10_000_000_000)
+            for s in random_trace(r, allow_npe=False):
+                tid = hi + lo if r.random() < 0.6 else lo
+                batch.append(s.to_builder(trace_id=tid, timestamp=ts0 + r.randrange(1_000_000)))
+        r.shuffle(batch)
+        out.append(batch)
+    return out
+
+
+@pytest.mark.parametrize("seed", range(15))
+@pytest.mark.parametrize("strict", [True, False])
+def test_no_arg_get_dependencies_vs_oracle(seed, strict):
+    """getDependencies() (IMS:265-270, ZipkinRule's): every trace, lowTraceId order, split by
+    the full trace id when strictTraceId; exact list order."""
+    store = InMemoryStorage(strict_trace_id=strict, max_span_count=80, compact_min=4)
+    ref = O.InMemoryStorage(strict_trace_id=strict, max_span_count=80)
+    for b in _mixed_width_batches(seed):
+        if len(b) > 80:
+            continue
+        store.accept(b).execute()
+        ref.accept(b)
+        assert _as_list(store.get_dependencies()) == _as_list(ref.get_dependencies_all())
+    store.close()
+
+
+def test_get_dependencies_snapshots_its_traces():
+    """The Call answers for the traces selected when getDependencies was called (the
+    reference's getTraces(request, false) runs inside getDependencies, IMS:323-332): later
+    accepts and clear() do not change it."""
+    b = _batches(3)
+    store = InMemoryStorage()
+    store.accept(b[0]).execute()
+    end_ms = (BASE_US + 10_000_000_000) // 1000 + 1000
+    call = store.get_dependencies(end_ms, 86_400_000 * 2)
+    ref = O.InMemoryStorage()
+    ref.accept(b[0])
+    store.accept(b[1]).execute()
+    store.clear()
+    assert _as_list(call.execute()) == _as_list(ref.get_dependencies(end_ms, 86_400_000 * 2))
+    store.close()

@@ -34,7 +34,7 @@ EXPORTS = (
     "zdl_link", "zdl_merge_links", "zdl_add_links", "zdl_reset", "zdl_table_export",
     "zdl_table_import", "zdl_get_kernel_times", "zdl_stream", "zdl_set_days", "zdl_link_days",
     "zdl_store_create", "zdl_store_destroy", "zdl_store_last_error", "zdl_store_append", "zdl_store_clear",
-    "zdl_store_size", "zdl_put_stored",
+    "zdl_store_size", "zdl_put_stored", "zdl_store_compact",
     "zdl_decoder_create", "zdl_decoder_destroy", "zdl_decoder_last_error", "zdl_decoder_bind",
     "zdl_decoder_dict_size", "zdl_decoder_missing", "zdl_decode_proto3", "zdl_decode_proto3_retry",
     "zdl_decoder_download", "zdl_decoder_kernel_ms", "zdl_put_mysql_rows", "zdl_rows_last_error",
@@ -145,6 +145,8 @@ def lib() -> C.CDLL:
     L.zdl_store_append.restype = C.c_int
     L.zdl_store_clear.argtypes = [vp]
     L.zdl_store_clear.restype = C.c_int
+    L.zdl_store_compact.argtypes = [vp, vp, u64]
+    L.zdl_store_compact.restype = C.c_int
     L.zdl_store_size.argtypes = [vp]
     L.zdl_store_size.restype = u64
     L.zdl_put_stored.argtypes = [vp, vp, vp, u64, vp, u64]
@@ -412,6 +414,13 @@ class Store:
 
     def clear(self) -> None:
         self._L.zdl_store_clear(self.h)
+
+    def compact(self, keep: np.ndarray) -> None:
+        """zdl_store_compact: keep the spans at these ascending positions, renumbered 0..n."""
+        k = np.ascontiguousarray(keep, np.uint32)
+        rc = self._L.zdl_store_compact(self.h, _ptr(k), len(k))
+        if rc != ZDL_OK:
+            raise ZdlError(rc, self._L.zdl_store_last_error(self.h).decode())
 
     def __len__(self) -> int:
         return int(self._L.zdl_store_size(self.h))

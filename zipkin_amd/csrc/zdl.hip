@@ -1441,6 +1441,52 @@ int zdl_store_append(zdl_store* st, const zdl_span_cols* col, uint64_t n) {
   return ZDL_OK;
 }
 
+int zdl_store_compact(zdl_store* st, const uint32_t* keep, uint64_t n_keep) {
+  if (!st || (n_keep && !keep)) return ZDL_EINVAL;
+  if (n_keep > st->n) return store_fail(st, ZDL_EINVAL, "zdl_store_compact: more positions than stored spans");
+  for (uint64_t i = 0; i < n_keep; ++i)
+    if (keep[i] >= st->n || (i && keep[i] <= keep[i - 1]))
+      return store_fail(st, ZDL_EINVAL, "zdl_store_compact: positions must ascend inside the store");
+  (void)hipGetLastError();
+  hipError_t e = hipSetDevice(st->device);
+  const hipStream_t s = st->stream;
+  const uint64_t cap = std::max<uint64_t>(2 * n_keep, 1 << 16);
+  DevBuf<uint64_t> id, pid;
+  DevBuf<int32_t> lsvc, rsvc, ip4, ip6;
+  DevBuf<uint32_t> pf, idx;
+  DevBuf<int64_t> ts;
+  if (e == hipSuccess) e = id.ensure(cap);
+  if (e == hipSuccess) e = pid.ensure(cap);
+  if (e == hipSuccess) e = lsvc.ensure(cap);
+  if (e == hipSuccess) e = rsvc.ensure(cap);
+  if (e == hipSuccess) e = ip4.ensure(cap);
+  if (e == hipSuccess) e = ip6.ensure(cap);
+  if (e == hipSuccess) e = pf.ensure(cap);
+  if (e == hipSuccess) e = ts.ensure(cap);
+  if (e == hipSuccess) e = idx.ensure(std::max<uint64_t>(n_keep, 1));
+  if (e == hipSuccess && n_keep) e = hipMemcpyAsync(idx.p, keep, n_keep * 4, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess && n_keep) {
+    const Cols in{st->id.p, st->pid.p, st->lsvc.p, st->rsvc.p, st->ip4.p, st->ip6.p, st->pf.p, st->ts.p};
+    hipLaunchKernelGGL(k_gather, dim3((unsigned)((n_keep + 255) / 256)), dim3(256), 0, s, in, idx.p, n_keep, id.p,
+                       pid.p, lsvc.p, rsvc.p, ip4.p, ip6.p, pf.p, ts.p);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    id.release(); pid.release(); lsvc.release(); rsvc.release(); ip4.release(); ip6.release(); pf.release();
+    ts.release(); idx.release();
+    return store_fail(st, e == hipErrorOutOfMemory ? ZDL_ENOMEM : ZDL_EDEVICE,
+                      std::string("zdl_store_compact: ") + hipGetErrorString(e));
+  }
+  st->id.release(); st->pid.release(); st->lsvc.release(); st->rsvc.release(); st->ip4.release();
+  st->ip6.release(); st->pf.release(); st->ts.release();
+  st->id = id; st->pid = pid; st->lsvc = lsvc; st->rsvc = rsvc; st->ip4 = ip4; st->ip6 = ip6; st->pf = pf; st->ts = ts;
+  idx.release();
+  st->n = n_keep;
+  st->cap = cap;
+  return ZDL_OK;
+}
+
 int zdl_put_stored(zdl_ctx* c, const zdl_store* st, const uint32_t* perm, uint64_t n_sel, const uint64_t* off,
                    uint64_t n_traces) {
   if (!c || !st || (n_sel && !perm) || !off) return fail(c, ZDL_EINVAL, "null argument");
