@@ -252,3 +252,20 @@ def test_comm_job_of_one_rank(config):
     again = sorted(_tuples(*ctx.link()))
     ctx.close()
     assert got == again == sorted(_oracle(cols))
+
+
+@pytest.mark.parametrize("exact", [False, True])
+def test_c5_body_big_trace_paths_vs_cpp(exact, monkeypatch):
+    """Traces above 64 spans: the sort-free path for simple ids (big_simple, LDS-resident up
+    to ~1600 spans, HBM scratch beyond) and the exact sorting path (ZDL_BIG_EXACT=1) both
+    equal the C++ restatement on C5's Pareto body (depth 64, fan-out <= 1000)."""
+    if exact:
+        monkeypatch.setenv("ZDL_BIG_EXACT", "1")
+    cols = synth.generate(synth.C5.scaled(200_000))
+    sizes = np.diff(cols.offsets.astype(np.int64))
+    assert (sizes > 64).sum() > 500 and (sizes > 2000).sum() > 5
+    ctx = N.Context(10_000)
+    ctx.put_spans(cols)
+    got = sorted(_tuples(*ctx.link()))
+    ctx.close()
+    assert got == sorted(_oracle(cols))

@@ -108,6 +108,10 @@ struct Args {
   int32_t* b_parent;
   uint8_t* b_live;
   uint8_t* b_haschild;
+  int skip_simple;            // ZDL_BIG_EXACT=1 (tests): every big trace takes the exact path
+  int32_t* b_nm;              // big_simple in HBM: nearest-kinded-ancestor pointers
+  unsigned long long* b_hk;   // big_simple in HBM: 2 hash slots per span (keys, then two u32 values)
+  uint32_t* b_hv;
   // insertion order (ZDL_FLAG_INSERTION_ORDER): first-addLink ranks per cell (ord_min),
   // the put-global position of this put's span 0, and big-trace breadth-first scratch
   unsigned long long* first;
@@ -270,8 +274,235 @@ __device__ __forceinline__ void big_bfs(const View& v, int n, int rp, unsigned l
   }
 }
 
+// ------------------------------------------------- big traces, simple ids (k_tail)
+// A trace longer than WSMALL whose ids are "simple" (per id at most one non-shared and one
+// shared span, the condition under which k_link's windows skip Trace.merge) is linked without
+// sorting: k_link's algorithm at workgroup scale, every phase one parallel loop and a barrier.
+//   1. (id) -> {non-shared, shared} index in a hash of exact 64-bit keys (2n slots, CAS);
+//      a second span with the same (id, shared) aborts to the exact (sorting) path;
+//   2. root = the non-shared parentless span with the smallest id (SpanNode.java:203-249 via
+//      DESIGN.md §3); tree parents by lookup of the parent id, the shared candidate first when
+//      its endpoint equals (SpanNode.Builder.process); Trace.merge's backfill of a shared span's
+//      parent id (Trace.java:76-79);
+//   3. reachability and firstRemoteAncestor (DependencyLinker.java:153-164) by pointer jumping
+//      (O(log depth) rounds; a cycle never reaches the root, as in SpanNode.traverse);
+//   4. DependencyLinker.java:58-148 per node, straight into the global tables.
+// The arrays live in the workgroup's LDS when the trace fits, else in HBM scratch at the
+// trace's span offset. Returns false (nothing counted) when the trace is not simple.
+struct BSView {
+  uint64_t* id;
+  uint64_t* pid;
+  int32_t* ls;
+  int32_t* rs;
+  int32_t* i4;
+  int32_t* i6;
+  uint32_t* pf;
+  int32_t* par;
+  int32_t* a;
+  int32_t* nm;
+  unsigned long long* hk;
+  uint32_t* hns;
+  uint32_t* hsh;
+  uint8_t* hasc;
+};
+constexpr size_t bs_bytes(int n) { return (size_t)n * (8 + 8 + 4 * 5 + 4 * 3 + 1) + (size_t)2 * n * (8 + 4 + 4) + 16 * 15; }  // + alignment of 14 arrays
+
+__device__ __forceinline__ int bs_slot(uint64_t key, int n) {
+  const uint32_t h = ((uint32_t)key ^ (uint32_t)(key >> 32)) * 0x9E3779B1u;
+  return (int)__umulhi(h, 2u * (uint32_t)n);
+}
+// The slot holding key (or the empty slot where it would go).
+__device__ __forceinline__ int bs_find(const BSView& v, uint64_t key, int n) {
+  int q = bs_slot(key, n);
+  while (true) {
+    const unsigned long long k = v.hk[q];
+    if (k == key || k == 0ull) return q;
+    q = q + 1 == 2 * n ? 0 : q + 1;
+  }
+}
+
+__device__ bool big_simple(const Args& A, unsigned char* lds, size_t lds_bytes, uint64_t b, int n, uint32_t day) {
+  __shared__ int sh_bad, sh_more;
+  __shared__ unsigned long long sh_rootid;
+  __shared__ int sh_rp;
+  BSView v;
+  if (bs_bytes(n) <= lds_bytes) {  // LDS
+    unsigned char* p = lds;
+    auto take = [&](size_t bytes) { unsigned char* r = p; p += (bytes + 15) & ~(size_t)15; return r; };
+    v.hk = (unsigned long long*)take((size_t)16 * n);
+    v.id = (uint64_t*)take((size_t)8 * n);
+    v.pid = (uint64_t*)take((size_t)8 * n);
+    v.hns = (uint32_t*)take((size_t)8 * n);
+    v.hsh = (uint32_t*)take((size_t)8 * n);
+    v.ls = (int32_t*)take((size_t)4 * n);
+    v.rs = (int32_t*)take((size_t)4 * n);
+    v.i4 = (int32_t*)take((size_t)4 * n);
+    v.i6 = (int32_t*)take((size_t)4 * n);
+    v.pf = (uint32_t*)take((size_t)4 * n);
+    v.par = (int32_t*)take((size_t)4 * n);
+    v.a = (int32_t*)take((size_t)4 * n);
+    v.nm = (int32_t*)take((size_t)4 * n);
+    v.hasc = (uint8_t*)take((size_t)n);
+  } else {  // HBM scratch at the trace's span offset (2 hash slots per span)
+    v.id = A.b_id + b;
+    v.pid = A.b_pid + b;
+    v.ls = A.b_lsvc + b;
+    v.rs = A.b_rsvc + b;
+    v.i4 = A.b_ip4 + b;
+    v.i6 = A.b_ip6 + b;
+    v.pf = A.b_pf + b;
+    v.par = A.b_parent + b;
+    v.a = (int32_t*)(A.b_perm + b);
+    v.nm = A.b_nm + b;
+    v.hasc = A.b_haschild + b;
+    v.hk = A.b_hk + 2 * b;
+    v.hns = A.b_hv + 4 * b;
+    v.hsh = A.b_hv + 4 * b + 2 * n;
+  }
+  if (threadIdx.x == 0) {
+    sh_bad = 0;
+    sh_rootid = ~0ull;
+    sh_rp = PAR_TERMINAL;
+  }
+  for (int i = threadIdx.x; i < 2 * n; i += BIG_WG) {
+    v.hk[i] = 0ull;
+    v.hns[i] = 0u;
+    v.hsh[i] = 0u;
+  }
+  for (int i = threadIdx.x; i < n; i += BIG_WG) {
+    const uint64_t g = b + i;
+    const uint64_t id = A.c.id[g];
+    const uint64_t pid = A.c.pid[g];
+    v.id[i] = id;
+    v.pid[i] = pid == id ? 0 : pid;  // Span.build drops a self parent (Span.java:611-617)
+    v.ls[i] = A.c.lsvc[g];
+    v.rs[i] = A.c.rsvc[g];
+    v.i4[i] = A.c.ip4[g];
+    v.i6[i] = A.c.ip6[g];
+    v.pf[i] = A.c.pf[g];
+    v.hasc[i] = 0;
+  }
+  __syncthreads();
+  // 1. the id hash; a second span with one (id, shared) -> not simple
+  for (int i = threadIdx.x; i < n; i += BIG_WG) {
+    const uint64_t id = v.id[i];
+    int q = bs_slot(id, n);
+    while (true) {
+      const unsigned long long old = atomicCAS(&v.hk[q], 0ull, (unsigned long long)id);
+      if (old == 0ull || old == id) break;
+      q = q + 1 == 2 * n ? 0 : q + 1;
+    }
+    const bool sh = is_shared(v.pf[i]);
+    if (atomicCAS(sh ? &v.hsh[q] : &v.hns[q], 0u, (uint32_t)i + 1u) != 0u) sh_bad = 1;
+    if ((uint32_t)v.ls[i] >= A.S && v.ls[i] >= 0) sh_bad = 2;
+    if ((uint32_t)v.rs[i] >= A.S && v.rs[i] >= 0) sh_bad = 2;
+    if (!sh && v.pid[i] == 0) atomicMin(&sh_rootid, (unsigned long long)id);
+  }
+  __syncthreads();
+  if (sh_bad == 2 && threadIdx.x == 0) atomicOr(A.status, ST_BADSVC);
+  if (sh_bad) {
+    __syncthreads();
+    return sh_bad == 2;  // bad service ids: counted nowhere, the put fails
+  }
+  if (threadIdx.x == 0 && sh_rootid != ~0ull) sh_rp = (int)v.hns[bs_find(v, sh_rootid, n)] - 1;
+  __syncthreads();
+  const int rp = sh_rp, root_attach = rp >= 0 ? rp : PAR_TERMINAL;
+  // 2. tree parents (+ the shared spans' parent-id backfill) and has-children
+  for (int i = threadIdx.x; i < n; i += BIG_WG) {
+    const uint32_t pf = v.pf[i];
+    int par;
+    if (is_shared(pf)) {
+      const int ns_own = (int)v.hns[bs_find(v, v.id[i], n)] - 1;
+      par = ns_own >= 0 ? ns_own : root_attach;
+      if (ns_own >= 0 && v.pid[i] == 0) v.pid[i] = v.pid[ns_own];  // Trace.java:76-79 (only shared pids change)
+    } else if (i == rp) {
+      par = PAR_TERMINAL;
+    } else if (v.pid[i] != 0) {
+      const uint64_t P = v.pid[i];
+      const int q = bs_find(v, P, n);
+      int nss = -1, shs = -1;
+      if (v.hk[q] == P) {
+        nss = (int)v.hns[q] - 1;
+        shs = (int)v.hsh[q] - 1;
+      }
+      const bool same_ep = shs >= 0 && v.ls[shs] == v.ls[i] && v.i4[shs] == v.i4[i] && v.i6[shs] == v.i6[i] &&
+                           port_of(v.pf[shs]) == port_of(pf);
+      par = same_ep ? shs : (nss >= 0 ? nss : root_attach);
+    } else {
+      par = root_attach;
+    }
+    v.par[i] = par;
+    v.a[i] = par;
+    v.nm[i] = par;
+    if (par >= 0) v.hasc[par] = 1;
+  }
+  __syncthreads();
+  // 3. pointer jumping: a -> PAR_TERMINAL iff reachable, nm -> nearest ancestor with a kind
+  int rounds = 4;
+  for (int m = n; m > 1; m >>= 1) rounds += 2;
+  for (int r = 0; r < rounds; ++r) {
+    if (threadIdx.x == 0) sh_more = 0;
+    __syncthreads();
+    bool more = false;
+    for (int i = threadIdx.x; i < n; i += BIG_WG) {
+      const int x = v.a[i];
+      if (x >= 0) {
+        v.a[i] = v.a[x];
+        more = true;
+      }
+      const int y = v.nm[i];
+      if (y >= 0 && kind_of(v.pf[y]) == ZDL_KIND_NULL) {
+        v.nm[i] = v.nm[y];
+        more = true;
+      }
+    }
+    if (more) sh_more = 1;
+    __syncthreads();
+    if (!sh_more) break;
+  }
+  // 4. DependencyLinker's rules per node (every span of a simple trace is a node)
+  for (int i = threadIdx.x; i < n; i += BIG_WG) {
+    if (v.a[i] != PAR_TERMINAL) continue;  // unreachable (a cycle not through the root)
+    const uint32_t pf = v.pf[i];
+    const uint32_t kind0 = kind_of(pf);
+    if (kind0 == ZDL_KIND_CLIENT && v.hasc[i]) continue;
+    const int32_t svc = v.ls[i], rsvc = v.rs[i];
+    uint32_t kind = kind0;
+    if (kind == ZDL_KIND_NULL) {
+      if (svc >= 0 && rsvc >= 0) kind = ZDL_KIND_CLIENT; else continue;
+    }
+    const bool srv = kind == ZDL_KIND_SERVER || kind == ZDL_KIND_CONSUMER;
+    int32_t pa = srv ? rsvc : svc;
+    const int32_t ch = srv ? svc : rsvc;
+    if (srv && i == rp && pa < 0) continue;
+    bool err = err_of(pf);
+    auto emit = [&](int32_t x, int32_t y, bool e) {
+      const size_t idx = ((size_t)day * A.S + (size_t)x) * A.S + y;
+      atomicAdd(&A.call[idx], 1ull);
+      if (e) atomicAdd(&A.err[idx], 1ull);
+    };
+    if (kind == ZDL_KIND_PRODUCER || kind == ZDL_KIND_CONSUMER) {
+      if (pa >= 0 && ch >= 0) emit(pa, ch, err);
+      continue;
+    }
+    const int ra = v.nm[i];
+    if (ra >= 0) {
+      const int32_t ran = v.ls[ra];
+      if (ran >= 0) {
+        if (kind == ZDL_KIND_CLIENT && svc >= 0 && ran != svc) emit(ran, svc, false);
+        if (kind == ZDL_KIND_SERVER || pa < 0) pa = ran;
+        const uint32_t apf = v.pf[ra];
+        if (!err && kind_of(apf) == ZDL_KIND_CLIENT && v.pid[i] != 0 && v.pid[i] == v.id[ra]) err = err_of(apf);
+      }
+    }
+    if (pa >= 0 && ch >= 0) emit(pa, ch, err);
+  }
+  __syncthreads();
+  return true;
+}
+
 template <int ORD>
-__device__ __forceinline__ void big_traces(const Args& A) {
+__device__ __forceinline__ void big_traces(const Args& A, unsigned char* lds, size_t lds_bytes) {
   __shared__ int32_t sh_root;
   __shared__ int sh_act;
   __shared__ int64_t sh_ts_root_idx, sh_ts_min;
@@ -375,6 +606,7 @@ __device__ __forceinline__ void big_traces(const Args& A) {
       if (sh_ts_min < 0) { big_sync(); continue; }
     }
     const uint32_t day = A.days ? (uint32_t)sh_ts_min : 0u;
+    if (!ORD && !A.skip_simple && big_simple(A, lds, lds_bytes, b, n, day)) continue;  // else the exact path
     // bitonic sort of perm by span_less (any n: out-of-range partners are +inf)
     int npad = 1;
     while (npad < n) npad <<= 1;
@@ -568,7 +800,7 @@ __global__ void __launch_bounds__(COMPACT_WG) k_compact_ordered(const unsigned l
 // table into the mapped host buffer, so zdl_link needs no kernel. Also zeroes the next
 // put's counters.
 static_assert(TAIL_WG == BIG_WG && TAIL_WG == COMPACT_WG, "k_tail runs all three parts");
-inline size_t tail_block_bytes(int window) { return WTABLE_BYTES + (TAIL_WG / 64) * wl::bytes(window); }
+constexpr size_t tail_block_bytes(int window) { return WTABLE_BYTES + (TAIL_WG / 64) * wl::bytes(window); }
 
 template <int DENSE, int WINDOW, int ORD>
 __global__ void __launch_bounds__(TAIL_WG, 1) k_tail(Args A) {
@@ -580,7 +812,7 @@ __global__ void __launch_bounds__(TAIL_WG, 1) k_tail(Args A) {
   }
   full_windows<DENSE, WINDOW, TAIL_WG / 64, ORD>(A, lds);
   __syncthreads();
-  big_traces<ORD>(A);
+  big_traces<ORD>(A, lds, tail_block_bytes(WINDOW));
   if (!A.map) return;
   // Hand-off to the last workgroup (MI355X_MICROARCH.md, "Valid forms", first table row):
   // the table and status updates are agent-scope atomics, performed at the memory side;
@@ -745,6 +977,10 @@ struct zdl_ctx {
   DevBuf<int32_t> b_lsvc, b_rsvc, b_ip4, b_ip6, b_parent;
   DevBuf<uint32_t> b_pf, b_perm;
   DevBuf<uint8_t> b_live, b_hasc;
+  DevBuf<int32_t> b_nm;
+  DevBuf<unsigned long long> b_hk;
+  DevBuf<uint32_t> b_hv;
+  int big_exact = 0;  // ZDL_BIG_EXACT=1: big traces skip big_simple (tests compare both paths)
   // host-API staging
   DevBuf<uint64_t> h_id, h_pid, h_off;
   DevBuf<int32_t> h_lsvc, h_rsvc, h_ip4, h_ip6;
@@ -969,6 +1205,8 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
     }
     const char* sk = getenv("ZDL_SKIP");
     c->skip = sk ? (uint32_t)strtoul(sk, nullptr, 0) : 0u;
+    const char* be = getenv("ZDL_BIG_EXACT");
+    c->big_exact = be && be[0] == '1';
     const char* ft = getenv("ZDL_TM");
     if (ft) c->force_tm = !strcmp(ft, "hash") ? TM_HASH : (!strcmp(ft, "log") ? TM_LOG : -1);
   }
@@ -1019,7 +1257,7 @@ void zdl_destroy(zdl_ctx* c) {
   c->tr_node.release(); c->tr_parent.release(); c->tr_bfs.release();
   c->b_id.release(); c->b_pid.release(); c->b_lsvc.release(); c->b_rsvc.release(); c->b_ip4.release();
   c->b_ip6.release(); c->b_parent.release(); c->b_pf.release(); c->b_perm.release(); c->b_live.release();
-  c->b_hasc.release();
+  c->b_hasc.release(); c->b_nm.release(); c->b_hk.release(); c->b_hv.release();
   c->h_id.release(); c->h_pid.release(); c->h_off.release(); c->h_lsvc.release(); c->h_rsvc.release();
   c->h_ip4.release(); c->h_ip6.release(); c->h_pf.release(); c->h_ts.release();
   c->h_lo.release(); c->h_ord.release(); c->grp.release(); c->lw.release();
@@ -1213,6 +1451,9 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   HIP_TRY(c, c->b_parent.ensure(n_spans));
   HIP_TRY(c, c->b_live.ensure(n_spans));
   HIP_TRY(c, c->b_hasc.ensure(n_spans));
+  HIP_TRY(c, c->b_nm.ensure(n_spans));
+  HIP_TRY(c, c->b_hk.ensure(2 * n_spans));
+  HIP_TRY(c, c->b_hv.ensure(4 * n_spans));
   A.b_id = c->b_id.p;
   A.b_pid = c->b_pid.p;
   A.b_lsvc = c->b_lsvc.p;
@@ -1224,6 +1465,10 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   A.b_parent = c->b_parent.p;
   A.b_live = c->b_live.p;
   A.b_haschild = c->b_hasc.p;
+  A.b_nm = c->b_nm.p;
+  A.b_hk = c->b_hk.p;
+  A.b_hv = c->b_hv.p;
+  A.skip_simple = c->big_exact;
   if (c->flags & ZDL_FLAG_TREE_EXPORT) {  // the last put's tree (insertion-order contexts only)
     HIP_TRY(c, c->tr_node.ensure(n_spans));
     HIP_TRY(c, c->tr_parent.ensure(n_spans));
