@@ -81,6 +81,10 @@ extern "C" {
                                         zdl_link can return ZDL_ORDER_INSERTION; puts take the exact
                                         per-trace path (slower than the default streaming path); traces
                                         are limited to 2^21 spans */
+#define ZDL_FLAG_DENSE_TABLE 16u     /* keep the S x S count table above 1024 services (a device group's
+                                        and a multi-process job's RCCL reduce sums those tables); without
+                                        it such a context keeps its links as one sorted list instead
+                                        (a sparse context: no 16 * S^2 bytes of tables, S <= 46340) */
 #define ZDL_FLAG_TREE_EXPORT 8u      /* with ZDL_FLAG_INSERTION_ORDER: every put also records the tree
                                         SpanNode.Builder builds (SpanNode.java:122-249), read back by
                                         zdl_tree_export (parity tests of the tree itself, not only its

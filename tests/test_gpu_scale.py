@@ -269,3 +269,61 @@ def test_c5_body_big_trace_paths_vs_cpp(exact, monkeypatch):
     got = sorted(_tuples(*ctx.link()))
     ctx.close()
     assert got == sorted(_oracle(cols))
+
+
+@pytest.mark.parametrize("config", ["c2", "c4"])
+def test_sparse_context_forced_small(config, monkeypatch):
+    """ZDL_SPARSE=1: the sorted-list table (zdl_sparse.h) at a small dictionary, against the
+    dense context and the restatement, over three puts (merge of lists) and a reset."""
+    monkeypatch.setenv("ZDL_SPARSE", "1")
+    w = synth.CONFIGS[config].scaled(100_000)
+    cols = synth.generate(w)
+    ctx = N.Context(w.total_services)
+    ctx.put_spans(cols)
+    one = sorted(_tuples(*ctx.link()))
+    ctx.put_spans(cols)
+    ctx.put_spans(cols)
+    three = sorted(_tuples(*ctx.link()))
+    ctx.reset()
+    assert len(ctx.link()[0]) == 0
+    ctx.put_spans(cols)
+    again = sorted(_tuples(*ctx.link()))
+    ctx.close()
+    exp = sorted(_oracle(cols))
+    assert one == exp == again
+    assert three == [(a, b, 3 * n, 3 * e) for a, b, n, e in exp]
+
+
+def test_sparse_vs_dense_table_large_dictionary():
+    """2000 services: sparse by default, the S x S table with ZDL_FLAG_DENSE_TABLE; with a
+    service rank table (sorted output by name order), a time window and add_links."""
+    w = synth.Workload("c5_like_2000", 0x5EED0077, 200_000, 2000, max_depth=32, size_dist=1, pareto_alpha=1.3,
+                       max_size=5000, max_fanout=200, zipf_s=1.1)
+    cols = synth.generate(w)
+    rank = np.random.default_rng(5).permutation(2000).astype(np.int32)
+    base_ms = w.base_ts_us // 1000
+    out = []
+    for dense in (False, True):
+        ctx = N.Context(2000, dense_table=dense)
+        ctx.set_ranks(N.ZDL_DICT_SERVICE, rank)
+        ctx.put_spans(cols)
+        full = _tuples(*ctx.link())
+        ctx.add_links(np.array([3, 3, 1999], np.int32), np.array([4, 4, 0], np.int32), np.array([5, 1, 2], np.int64),
+                      np.array([1, 0, 2], np.int64))
+        added = _tuples(*ctx.link())
+        ctx.reset()
+        ctx.set_window(base_ms + 120_000, 60_000)
+        ctx.put_spans(cols)
+        windowed = _tuples(*ctx.link())
+        ctx.close()
+        out.append((full, added, windowed))
+    assert out[0] == out[1]  # the same links in the same (rank) order
+    full, added, windowed = out[0]
+    assert sorted(full) == sorted(_oracle(cols))
+    assert [(rank[p], rank[c]) for p, c, _, _ in full] == sorted((rank[p], rank[c]) for p, c, _, _ in full)
+    st, p, c, n, e = ref.link(cols, window=(base_ms + 120_000, 60_000), threads=16)
+    assert st == 0 and sorted(windowed) == sorted(_tuples(p, c, n, e))
+    d = {(a, b): (x, y) for a, b, x, y in full}
+    for a, b, x, y in ((3, 4, 6, 1), (1999, 0, 2, 2)):
+        x0, y0 = d.get((a, b), (0, 0))
+        assert (a, b, x0 + x, y0 + y) in added

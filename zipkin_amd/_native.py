@@ -18,6 +18,7 @@ ZDL_FLAG_TIMING = 1
 ZDL_FLAG_TIMING_ALL = 2
 ZDL_FLAG_INSERTION_ORDER = 4
 ZDL_FLAG_TREE_EXPORT = 8
+ZDL_FLAG_DENSE_TABLE = 16
 ZDL_AKEY_NONE, ZDL_AKEY_LC, ZDL_AKEY_CA, ZDL_AKEY_CS, ZDL_AKEY_SA, ZDL_AKEY_SR, ZDL_AKEY_ERROR = range(7)
 
 PF_KIND_SHIFT = 16
@@ -205,13 +206,14 @@ class Context:
 
     def __init__(self, n_services: int, device: int = 0, timing: bool = False, timing_all: bool = False,
                  timing_stride: int = 1, insertion_order: bool = False, device_ids=None,
-                 tree_export: bool = False):
+                 tree_export: bool = False, dense_table: bool = False):
         """device_ids: a device group (zdl_config.device_ids): traces sharded over these GPUs,
         the tables summed by RCCL at link()."""
         L = lib()
         flags = (ZDL_FLAG_TIMING if timing else 0) | (ZDL_FLAG_TIMING_ALL if timing_all else 0)
         flags |= ZDL_FLAG_INSERTION_ORDER if insertion_order else 0
         flags |= ZDL_FLAG_TREE_EXPORT if tree_export else 0
+        flags |= ZDL_FLAG_DENSE_TABLE if dense_table else 0
         ids = None
         if device_ids is not None:
             ids = (C.c_int32 * len(device_ids))(*[int(d) for d in device_ids])

@@ -18,6 +18,8 @@
 
 #include "zdl_group.h"
 
+#include <hipcub/hipcub.hpp>
+
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -28,6 +30,7 @@
 
 #include "../../include/zdl.h"
 #include "zdl_algo.h"
+#include "zdl_sparse.h"
 
 namespace zdl {
 
@@ -54,6 +57,9 @@ constexpr int PSHIFT = 12;          // cells per partition: 4096 u64 LDS cells =
 constexpr int PMAX = 256;           // partitions (per-wave LDS counters in k_link): S <= 1024
 // k_link's table modes (template parameter DENSE): hash, dense, log
 constexpr int TM_HASH = 0, TM_DENSE = 1, TM_LOG = 2;
+// SORT (sparse contexts, zdl_sparse.h): k_link logs every link like LOG, without partition
+// counts; the put's log is sorted and merged into the context's sorted link list
+constexpr int TM_SORT = 3;
 
 struct Cols {
   const uint64_t* id;
@@ -139,6 +145,12 @@ struct Args {
   int32_t* tr_node;
   int32_t* tr_parent;
   int32_t* tr_bfs;
+  // sparse contexts (zdl_sparse.h): k_tail's links go to log segments in tlg (2 entries per
+  // span: at 2 * the trace's / window's first span); tseg_big[bi] / tseg_win[k] = their counts
+  int sparse;
+  uint32_t* tlg;
+  uint32_t* tseg_big;
+  uint32_t* tseg_win;
 };
 
 #include "zdl_full.inc"  // the full per-window emulation (k_tail's first part)
@@ -321,7 +333,8 @@ __device__ __forceinline__ int bs_find(const BSView& v, uint64_t key, int n) {
   }
 }
 
-__device__ bool big_simple(const Args& A, unsigned char* lds, size_t lds_bytes, uint64_t b, int n, uint32_t day) {
+__device__ bool big_simple(const Args& A, unsigned char* lds, size_t lds_bytes, uint64_t b, int n, uint32_t day,
+                           uint32_t* scnt) {
   __shared__ int sh_bad, sh_more;
   __shared__ unsigned long long sh_rootid;
   __shared__ int sh_rp;
@@ -478,6 +491,10 @@ __device__ bool big_simple(const Args& A, unsigned char* lds, size_t lds_bytes, 
     bool err = err_of(pf);
     auto emit = [&](int32_t x, int32_t y, bool e) {
       const size_t idx = ((size_t)day * A.S + (size_t)x) * A.S + y;
+      if (A.sparse) {  // the trace's log segment
+        A.tlg[2 * b + atomicAdd(scnt, 1u)] = ((uint32_t)idx << 1) | (e ? 1u : 0u);
+        return;
+      }
       atomicAdd(&A.call[idx], 1ull);
       if (e) atomicAdd(&A.err[idx], 1ull);
     };
@@ -503,6 +520,7 @@ __device__ bool big_simple(const Args& A, unsigned char* lds, size_t lds_bytes, 
 
 template <int ORD>
 __device__ __forceinline__ void big_traces(const Args& A, unsigned char* lds, size_t lds_bytes) {
+  __shared__ uint32_t sh_cnt;  // sparse: links logged for the current trace
   __shared__ int32_t sh_root;
   __shared__ int sh_act;
   __shared__ int64_t sh_ts_root_idx, sh_ts_min;
@@ -525,6 +543,8 @@ __device__ __forceinline__ void big_traces(const Args& A, unsigned char* lds, si
     v.live = A.b_live + b;
     v.haschild = A.b_haschild + b;
     if (threadIdx.x == 0) {
+      sh_cnt = 0;
+      if (A.sparse) A.tseg_big[bi] = 0;  // a trace skipped below logs nothing
       sh_root = 0x7fffffff;
       sh_act = 1;
       sh_ts_root_idx = 0x7fffffffffffffffll;
@@ -606,7 +626,10 @@ __device__ __forceinline__ void big_traces(const Args& A, unsigned char* lds, si
       if (sh_ts_min < 0) { big_sync(); continue; }
     }
     const uint32_t day = A.days ? (uint32_t)sh_ts_min : 0u;
-    if (!ORD && !A.skip_simple && big_simple(A, lds, lds_bytes, b, n, day)) continue;  // else the exact path
+    if (!ORD && !A.skip_simple && big_simple(A, lds, lds_bytes, b, n, day, &sh_cnt)) {  // else the exact path
+      if (A.sparse && threadIdx.x == 0) A.tseg_big[bi] = sh_cnt;
+      continue;
+    }
     // bitonic sort of perm by span_less (any n: out-of-range partners are +inf)
     int npad = 1;
     while (npad < n) npad <<= 1;
@@ -694,12 +717,17 @@ __device__ __forceinline__ void big_traces(const Args& A, unsigned char* lds, si
       link_node(v, p, rp, n, [&](int32_t a, int32_t c, bool e, int k) {
         if ((uint32_t)a >= A.S || (uint32_t)c >= A.S) { atomicOr(A.status, ST_BADSVC); return; }
         const size_t idx = ((size_t)day * A.S + (size_t)a) * A.S + c;  // row day * S + parent
+        if (A.sparse) {
+          A.tlg[2 * b + atomicAdd(&sh_cnt, 1u)] = ((uint32_t)idx << 1) | (e ? 1u : 0u);
+          return;
+        }
         atomicAdd(&A.call[idx], 1ull);
         if (e) atomicAdd(&A.err[idx], 1ull);
         if (ORD) ord_min(&A.first[idx], ord_rank(A.span_base + b, bfs[p], k));
       });
     }
     big_sync();
+    if (A.sparse && threadIdx.x == 0) A.tseg_big[bi] = sh_cnt;
   }
 }
 
@@ -836,7 +864,8 @@ __global__ void __launch_bounds__(TAIL_WG, 1) k_tail(Args A) {
   }
 }
 
-inline const void* k_tail_fn(int dense, int window, int ord = 0) {
+inline const void* k_tail_fn(int dense, int window, int ord = 0) {  // dense: 0 hash, 1 dense, 2 sparse sink
+  if (dense == 2) return window ? (const void*)k_tail<2, 1, 0> : (const void*)k_tail<2, 0, 0>;
   if (window == 2) {  // daily buckets
     if (ord) return dense ? (const void*)k_tail<1, 2, 1> : (const void*)k_tail<0, 2, 1>;
     return dense ? (const void*)k_tail<1, 2, 0> : (const void*)k_tail<0, 2, 0>;
@@ -961,6 +990,14 @@ struct zdl_ctx {
   DevBuf<uint64_t> lg_start;
   int force_tm = -1;  // ZDL_TM=hash|dense|log (tests / ablation): k_link's table mode when it fits
   DevBuf<int32_t> tr_node, tr_parent, tr_bfs;  // ZDL_FLAG_TREE_EXPORT: the last put's tree
+  // sparse contexts (zdl_sparse.h): the accumulated links as one list sorted by cell; per put
+  // the log segments of k_link and k_tail are gathered (seg_*) into lin and merged
+  bool sparse = false;
+  SparseTable acc;
+  SparseWork sw;
+  DevBuf<uint64_t> seg_src;
+  DevBuf<uint32_t> seg_n, seg_off, tseg_big, tseg_win, lin;
+  DevBuf<unsigned char> seg_tmp;
   uint64_t tr_n = 0;
   // Multi-GPU. A device group (zdl_config.device_ids): one context per device,
   // traces sharded by splitmix64(trace_lo) % n, the tables summed by RCCL (ncclReduce to the
@@ -1150,6 +1187,14 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
   c->S = cfg->n_services;
   c->flags = cfg->flags;
   c->ord = (cfg->flags & ZDL_FLAG_INSERTION_ORDER) != 0;
+  // a sorted link list instead of the S x S table above 1024 services (zdl_sparse.h); cells
+  // and keys are u32 (cell << 1 | error), so S <= 46340. ZDL_SPARSE=1/0 forces it (tests).
+  {
+    const char* sp = getenv("ZDL_SPARSE");
+    const bool want = sp ? sp[0] == '1' : cfg->n_services > 1024;
+    c->sparse = want && cfg->n_services <= 46340u &&
+                !(cfg->flags & (ZDL_FLAG_INSERTION_ORDER | ZDL_FLAG_DENSE_TABLE));
+  }
   if ((cfg->flags & ZDL_FLAG_TREE_EXPORT) && !c->ord) {
     delete c;
     g_create_error = "ZDL_FLAG_TREE_EXPORT needs ZDL_FLAG_INSERTION_ORDER (the exact per-trace path)";
@@ -1159,13 +1204,13 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
   c->lk_stride = std::max<uint32_t>(1u, cfg->timing_stride);
   hipError_t e = hipSetDevice(c->device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
-  const size_t SS = (size_t)c->S * c->S;
-  if (e == hipSuccess) e = c->call.ensure(SS);
-  if (e == hipSuccess) e = c->errc.ensure(SS);
+  const size_t SS = c->sparse ? 0 : (size_t)c->S * c->S;  // sparse: no S x S table
+  if (e == hipSuccess && SS) e = c->call.ensure(SS);
+  if (e == hipSuccess && SS) e = c->errc.ensure(SS);
   if (e == hipSuccess) e = c->status.ensure(4);
   if (e == hipSuccess) e = c->count.ensure(1);
-  if (e == hipSuccess) e = hipMemsetAsync(c->call.p, 0, SS * 8, c->stream);
-  if (e == hipSuccess) e = hipMemsetAsync(c->errc.p, 0, SS * 8, c->stream);
+  if (e == hipSuccess && SS) e = hipMemsetAsync(c->call.p, 0, SS * 8, c->stream);
+  if (e == hipSuccess && SS) e = hipMemsetAsync(c->errc.p, 0, SS * 8, c->stream);
   if (e == hipSuccess) e = hipMemsetAsync(c->status.p, 0, 16, c->stream);
   if (e == hipSuccess && c->ord) e = c->first.ensure(SS);
   if (e == hipSuccess && c->ord) e = hipMemsetAsync(c->first.p, 0xff, SS * 8, c->stream);
@@ -1255,6 +1300,8 @@ void zdl_destroy(zdl_ctx* c) {
   c->lg.release(); c->lg_grp.release(); c->lg_n.release(); c->lg_cnt.release(); c->lg_tot.release();
   c->lg_start.release();
   c->tr_node.release(); c->tr_parent.release(); c->tr_bfs.release();
+  c->acc.release(); c->sw.release(); c->seg_src.release(); c->seg_n.release(); c->seg_off.release();
+  c->tseg_big.release(); c->tseg_win.release(); c->lin.release(); c->seg_tmp.release();
   c->b_id.release(); c->b_pid.release(); c->b_lsvc.release(); c->b_rsvc.release(); c->b_ip4.release();
   c->b_ip6.release(); c->b_parent.release(); c->b_pf.release(); c->b_perm.release(); c->b_live.release();
   c->b_hasc.release(); c->b_nm.release(); c->b_hk.release(); c->b_hv.release();
@@ -1306,6 +1353,7 @@ int zdl_set_ranks(zdl_ctx* c, int dict, const int32_t* rank, uint32_t n) {
 int zdl_set_days(zdl_ctx* c, int64_t day0_ms, uint32_t n_days) {
   if (!c) return ZDL_EINVAL;
   if (!c->sub.empty() || c->comm) return fail(c, ZDL_EINVAL, "zdl_set_days: one device, one process");
+  if (c->sparse) return fail(c, ZDL_EINVAL, "zdl_set_days: needs the S x S table (a sparse context has none)");
   if (n_days > 255) return fail(c, ZDL_EINVAL, "zdl_set_days: at most 255 days");
   if (n_days && (day0_ms % DAY_MS) != 0) return fail(c, ZDL_EINVAL, "zdl_set_days: day0 must be a UTC midnight");
   if (n_days && c->window) return fail(c, ZDL_EINVAL, "zdl_set_days: not with a time window");
@@ -1371,6 +1419,76 @@ static hipError_t ensure_map(zdl_ctx* c) {
 // Insertion order and daily buckets: k_link only plans (mode 3), k_tail counts every window.
 static bool plan_only_mode(const zdl_ctx* c) { return c->ord || c->days; }
 
+// Sparse contexts: the segments (k_link's waves, then k_tail's big traces and queued windows)
+// listed with their start in lg and their link count.
+__global__ void k_seg_build(const uint64_t* __restrict__ lg_start, const uint32_t* __restrict__ lg_n, uint32_t W,
+                            const uint32_t* __restrict__ big_list, const uint64_t* __restrict__ off,
+                            const uint32_t* __restrict__ tseg_big, uint32_t nb, const uint64_t* __restrict__ cx_win,
+                            const uint32_t* __restrict__ tseg_win, uint32_t nw, uint64_t tbase,
+                            uint64_t* __restrict__ src, uint32_t* __restrict__ cnt) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < W) {
+    src[i] = lg_start[i];
+    cnt[i] = lg_n[i];
+  } else if (i < (uint64_t)W + nb) {
+    const uint32_t bi = (uint32_t)(i - W);
+    src[i] = tbase + 2 * off[big_list[bi]];
+    cnt[i] = tseg_big[bi];
+  } else if (i < (uint64_t)W + nb + nw) {
+    const uint64_t k = i - W - nb;
+    src[i] = tbase + 2 * (cx_win[2 * k] & ((1ull << 48) - 1));
+    cnt[i] = tseg_win[k];
+  }
+}
+
+__global__ void k_seg_copy(const uint32_t* __restrict__ lg, const uint64_t* __restrict__ src,
+                           const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ at, uint64_t nseg,
+                           uint32_t* __restrict__ lin) {
+  for (uint64_t sgm = blockIdx.x; sgm < nseg; sgm += gridDim.x) {
+    const uint32_t n = cnt[sgm];
+    const uint32_t* in = lg + src[sgm];
+    uint32_t* out = lin + at[sgm];
+    for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) out[j] = in[j];
+  }
+}
+
+static int sparse_finish(zdl_ctx* c, uint32_t ep, uint32_t lW, uint64_t n_spans, uint64_t n_traces,
+                         const uint64_t* off) {
+  const hipStream_t s = c->stream;
+  // how many big traces and queued windows k_tail logged (this put's counter slots)
+  HIP_TRY(c, hipMemcpyAsync(c->h_meta, c->counters.p + ep, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipMemcpyAsync((uint32_t*)c->h_meta + 1, c->counters.p + 2 + ep, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipStreamSynchronize(s));
+  const uint32_t nb = ((uint32_t*)c->h_meta)[0], nw = ((uint32_t*)c->h_meta)[1];
+  if (nb > n_traces || nw > n_traces) return fail(c, ZDL_EDEVICE, "sparse: inconsistent tail counters");
+  const uint64_t nseg = (uint64_t)lW + nb + nw;
+  HIP_TRY(c, c->seg_src.ensure(nseg));
+  HIP_TRY(c, c->seg_n.ensure(nseg));
+  HIP_TRY(c, c->seg_off.ensure(nseg));
+  hipLaunchKernelGGL(k_seg_build, dim3((unsigned)((nseg + 255) / 256)), dim3(256), 0, s, c->lg_start.p, c->lg_n.p, lW,
+                     c->big_list.p, off, c->tseg_big.p, nb, c->cx_win.p, c->tseg_win.p, nw, (uint64_t)2 * n_spans,
+                     c->seg_src.p, c->seg_n.p);
+  HIP_TRY(c, hipGetLastError());
+  size_t need = 0;
+  HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(nullptr, need, c->seg_n.p, c->seg_off.p, (int)nseg, s));
+  HIP_TRY(c, c->seg_tmp.ensure(need));
+  HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(c->seg_tmp.p, need, c->seg_n.p, c->seg_off.p, (int)nseg, s));
+  HIP_TRY(c, hipMemcpyAsync(c->h_meta, c->seg_off.p + (nseg - 1), 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipMemcpyAsync((uint32_t*)c->h_meta + 1, c->seg_n.p + (nseg - 1), 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipStreamSynchronize(s));
+  const uint64_t E = (uint64_t)((uint32_t*)c->h_meta)[0] + ((uint32_t*)c->h_meta)[1];
+  if (E > 4 * n_spans) return fail(c, ZDL_EDEVICE, "sparse: more links than the log holds");
+  if (E == 0) return ZDL_OK;
+  HIP_TRY(c, c->lin.ensure(E));
+  hipLaunchKernelGGL(k_seg_copy, dim3((unsigned)std::min<uint64_t>(nseg, 65536)), dim3(256), 0, s, c->lg.p,
+                     c->seg_src.p, c->seg_n.p, c->seg_off.p, nseg, c->lin.p);
+  HIP_TRY(c, hipGetLastError());
+  int kb = 1;
+  while ((1ull << kb) < (uint64_t)c->S * c->S) ++kb;
+  HIP_TRY(c, sparse_accumulate(c->sw, c->acc, c->lin.p, E, kb + 1, s));
+  return ZDL_OK;
+}
+
 // Default pipeline: k_link streams every trace of <= WSMALL spans; k_tail re-runs the
 // windows it queued, takes the traces it listed as longer than WSMALL and (small tables)
 // compacts the table into the mapped buffer zdl_link reads.
@@ -1386,6 +1504,10 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   if (c->force_tm == TM_LOG && SS <= ((size_t)PMAX << PSHIFT) && n_spans < (1ull << 31)) tm = TM_LOG;
   const bool plan_only = plan_only_mode(c);  // k_link mode 3: k_tail counts every window
   if (plan_only) tm = dense ? TM_DENSE : TM_HASH;
+  if (c->sparse) {  // every link to a log, sorted and merged after k_tail (zdl_sparse.h)
+    if (n_spans >= (1ull << 30)) return fail(c, ZDL_EINVAL, "sparse context: a put holds at most 2^30 spans");
+    tm = TM_SORT;
+  }
   const int grid = c->grid, lgrid = c->cus * lk::wgs_per_cu;  // k_link: two 16-wave workgroups per CU
   HIP_TRY(c, c->big_list.ensure(n_traces));
   // queued windows: at most one per trace; mode 3 (insertion order) uses one slot per trace
@@ -1424,6 +1546,20 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   A.prof = c->prof.p;
   const uint32_t lW = (uint32_t)lgrid * (uint32_t)lk::waves(c->window);
   const uint32_t lP = (uint32_t)((SS + (1u << PSHIFT) - 1) >> PSHIFT);
+  if (tm == TM_SORT) {  // k_link's segments in [0, 2n), k_tail's in [2n, 4n)
+    HIP_TRY(c, c->lg.ensure(4 * n_spans));
+    HIP_TRY(c, c->lg_start.ensure(lW));
+    HIP_TRY(c, c->lg_n.ensure(lW));
+    HIP_TRY(c, c->tseg_big.ensure(n_traces));
+    HIP_TRY(c, c->tseg_win.ensure(std::min<uint64_t>(n_traces, n_spans)));
+    A.lg = c->lg.p;
+    A.lg_start = c->lg_start.p;
+    A.lg_n = c->lg_n.p;
+    A.sparse = 1;
+    A.tlg = c->lg.p + 2 * n_spans;
+    A.tseg_big = c->tseg_big.p;
+    A.tseg_win = c->tseg_win.p;
+  }
   if (tm == TM_LOG) {
     HIP_TRY(c, c->lg.ensure(2 * n_spans));
     HIP_TRY(c, c->lg_grp.ensure(2 * n_spans));
@@ -1493,7 +1629,7 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
     A.o_fb = c->o_fb.p;
     A.o_bfs = c->o_bfs.p;
   }
-  const bool ordered = SS <= (size_t)COMPACT_WG * 8 && !c->ord && !c->days;
+  const bool ordered = SS <= (size_t)COMPACT_WG * 8 && !c->ord && !c->days && !c->sparse;
   if (ordered) HIP_TRY(c, ensure_map(c));
   A.map = ordered && !getenv("ZDL_NOTAILMAP") ? c->d_map : nullptr;
   A.done = c->counters.p + 4;
@@ -1526,8 +1662,8 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   ev_record(c, 2);
   ev_record(c, 3);
   c->map_fresh = false;  // k_link has changed the table
-  const hipError_t le = hipLaunchKernel(k_tail_fn(dense, wmode, c->ord ? 1 : 0), dim3(grid), dim3(TAIL_WG), kargs,
-                                        tail_block_bytes(wmode), c->stream);
+  const hipError_t le = hipLaunchKernel(k_tail_fn(c->sparse ? 2 : dense, wmode, c->ord ? 1 : 0), dim3(grid),
+                                        dim3(TAIL_WG), kargs, tail_block_bytes(wmode), c->stream);
   if (le != hipSuccess) {
     // k_link ran but k_tail did not: the counter slots are not re-zeroed and the table
     // holds part of the put. Mark the context: every put and link fails until zdl_reset.
@@ -1535,6 +1671,15 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
     return hip_fail(c, le, "k_tail launch");
   }
   if (A.map) c->seq = A.seq;
+  if (c->sparse) {  // gather the put's log segments, sort, reduce and merge into the list
+    const int rc = sparse_finish(c, ep, lW, n_spans, n_traces, off);
+    if (rc != ZDL_OK) {
+      c->span_base += n_spans;
+      ++c->epoch;
+      c->map_fresh = false;
+      return rc;
+    }
+  }
   c->span_base += n_spans;  // the next put's traces come after this one's
   ev_record(c, 4);
   ++c->epoch;  // k_tail zeroed the other counter slots
@@ -1876,9 +2021,10 @@ int zdl_reset(zdl_ctx* c) {
     HIP_TRY(c, hipMemsetAsync(c->counters.p, 0, 20, c->stream));
     c->poisoned = false;
   }
-  const size_t SS = (size_t)c->rows * c->S;
-  hipLaunchKernelGGL(k_zero_tables, dim3((unsigned)((SS + 255) / 256)), dim3(256), 0, c->stream, c->call.p,
-                     c->errc.p, (uint64_t)SS, c->status.p, c->ord ? c->first.p : nullptr);
+  const size_t SS = c->sparse ? 0 : (size_t)c->rows * c->S;  // sparse: only the status word
+  c->acc.n = 0;
+  hipLaunchKernelGGL(k_zero_tables, dim3((unsigned)std::max<size_t>((SS + 255) / 256, 1)), dim3(256), 0, c->stream,
+                     c->call.p, c->errc.p, (uint64_t)SS, c->status.p, c->ord ? c->first.p : nullptr);
   c->span_base = 0;
   if (c->days) HIP_TRY(c, hipMemsetAsync(c->day_first.p, 0xff, (size_t)c->days * 8, c->stream));
   HIP_TRY(c, hipGetLastError());
@@ -1961,6 +2107,8 @@ static int link_insertion(zdl_ctx* c, zdl_links* out) {
 
 }  // extern "C"
 
+static int ensure_rec(zdl_ctx* c, uint64_t m);
+
 // zdl_link's sorted output from the S x S tables (call, err) on c's device: c's own tables
 // (own: k_tail may already have compacted them into the mapped buffer) or summed ones (a
 // device group's or a multi-process job's reduction).
@@ -2013,16 +2161,8 @@ static int link_sorted(zdl_ctx* c, const unsigned long long* call, const unsigne
     // written straight into mapped pinned host columns sized by the link count
     uint64_t m = 0;
     HIP_TRY(c, compact_select(c->lw, call, SS, &m, c->stream));
-    if (m > c->h_rec_cap) {
-      if (c->h_rec) (void)hipHostFree(c->h_rec);
-      c->h_rec = nullptr;
-      c->d_rec = nullptr;
-      c->h_rec_cap = 0;
-      const size_t cap = std::max<size_t>((size_t)(m + m / 2 + 1) & ~(size_t)1, 1024);
-      HIP_TRY(c, hipHostMalloc((void**)&c->h_rec, cap * 24, hipHostMallocMapped | hipHostMallocCoherent));
-      HIP_TRY(c, hipHostGetDevicePointer((void**)&c->d_rec, c->h_rec, 0));
-      c->h_rec_cap = cap;
-    }
+    const int erc = ensure_rec(c, m);
+    if (erc != ZDL_OK) return erc;
     const size_t cap = c->h_rec_cap;
     HIP_TRY(c, compact_records(c->lw, call, err, m, c->S, c->nrank[0] ? c->rank[0].p : nullptr, c->nrank[0],
                                (int32_t*)c->d_rec, (int32_t*)(c->d_rec + 4 * cap), (int64_t*)(c->d_rec + 8 * cap),
@@ -2052,6 +2192,42 @@ static int link_sorted(zdl_ctx* c, const unsigned long long* call, const unsigne
 }
 
 static int comm_sum_tables(zdl_ctx* c);  // multi-process job: every rank's tables summed (below)
+
+// The mapped pinned output columns (parent, child i32; call, err i64) for m links.
+static int ensure_rec(zdl_ctx* c, uint64_t m) {
+  if (m <= c->h_rec_cap) return ZDL_OK;
+  if (c->h_rec) (void)hipHostFree(c->h_rec);
+  c->h_rec = nullptr;
+  c->d_rec = nullptr;
+  c->h_rec_cap = 0;
+  const size_t cap = std::max<size_t>((size_t)(m + m / 2 + 1) & ~(size_t)1, 1024);
+  HIP_TRY(c, hipHostMalloc((void**)&c->h_rec, cap * 24, hipHostMallocMapped | hipHostMallocCoherent));
+  HIP_TRY(c, hipHostGetDevicePointer((void**)&c->d_rec, c->h_rec, 0));
+  c->h_rec_cap = cap;
+  return ZDL_OK;
+}
+
+// A sparse context's links: its sorted list (cell = id order), rank-sorted when ranks are set.
+static int link_sparse(zdl_ctx* c, zdl_links* out) {
+  const uint64_t m = c->acc.n;
+  int rc = ensure_rec(c, m);
+  if (rc != ZDL_OK) return rc;
+  const size_t cap = c->h_rec_cap;
+  HIP_TRY(c, compact_sparse(c->lw, c->acc.cell, c->acc.call, c->acc.err, m, c->S,
+                            c->nrank[0] ? c->rank[0].p : nullptr, c->nrank[0], (int32_t*)c->d_rec,
+                            (int32_t*)(c->d_rec + 4 * cap), (int64_t*)(c->d_rec + 8 * cap),
+                            (int64_t*)(c->d_rec + 16 * cap), c->stream));
+  HIP_TRY(c, hipMemcpyAsync(c->h_meta, c->status.p, 16, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  rc = status_code(c, (uint32_t)c->h_meta[0]);
+  if (rc != ZDL_OK) return rc;
+  out->n = m;
+  out->parent = (const int32_t*)c->h_rec;
+  out->child = (const int32_t*)(c->h_rec + 4 * cap);
+  out->call_count = (const int64_t*)(c->h_rec + 8 * cap);
+  out->error_count = (const int64_t*)(c->h_rec + 16 * cap);
+  return ZDL_OK;
+}
 static int group_link(zdl_ctx* g, int order, zdl_links* out);
 
 extern "C" {
@@ -2068,6 +2244,7 @@ int zdl_link(zdl_ctx* c, int order, zdl_links* out) {
   }
   if (order != ZDL_ORDER_SORTED) return fail(c, ZDL_EINVAL, "zdl_link: order must be ZDL_ORDER_SORTED or ZDL_ORDER_INSERTION");
   HIP_TRY(c, enter(c));
+  if (c->sparse) return link_sparse(c, out);
   if (c->comm) {  // a rank of a multi-process job: the links of every rank's tables
     const int rc = comm_sum_tables(c);
     if (rc != ZDL_OK) return rc;
@@ -2264,6 +2441,25 @@ int zdl_add_links(zdl_ctx* c, const int32_t* parent, const int32_t* child, const
   if (c->days) return fail(c, ZDL_EINVAL, "zdl_add_links: not with daily buckets");
   if (n == 0) return ZDL_OK;
   HIP_TRY(c, enter(c));
+  if (c->sparse) {  // merged into the sorted list (DependencyLinker.merge's sum per pair)
+    std::vector<uint32_t> cells(n);
+    for (uint64_t i = 0; i < n; ++i) {
+      if ((uint32_t)parent[i] >= c->S || (uint32_t)child[i] >= c->S) return fail(c, ZDL_EINVAL, "service id >= n_services");
+      cells[i] = (uint32_t)parent[i] * c->S + (uint32_t)child[i];
+    }
+    hipStream_t s = c->stream;
+    HIP_TRY(c, c->lin.ensure(n));
+    HIP_TRY(c, c->mi_call.ensure(n));
+    HIP_TRY(c, c->mi_err.ensure(n));
+    HIP_TRY(c, hipMemcpyAsync(c->lin.p, cells.data(), n * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(c, hipMemcpyAsync(c->mi_call.p, call_count, n * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(c, hipMemcpyAsync(c->mi_err.p, error_count, n * 8, hipMemcpyHostToDevice, s));
+    int kb = 1;
+    while ((1ull << kb) < (uint64_t)c->S * c->S) ++kb;
+    HIP_TRY(c, sparse_add(c->sw, c->acc, c->lin.p, (const unsigned long long*)c->mi_call.p,
+                          (const unsigned long long*)c->mi_err.p, n, kb, s));
+    return zdl_sync(c);
+  }
   const uint64_t SS = (uint64_t)c->S * c->S;
   HIP_TRY(c, c->m_first.ensure(SS));
   HIP_TRY(c, c->mi_p.ensure(n));
@@ -2287,6 +2483,7 @@ int zdl_add_links(zdl_ctx* c, const int32_t* parent, const int32_t* child, const
 int zdl_table_export(zdl_ctx* c, void* dev_call, void* dev_err) {
   if (!c || !dev_call || !dev_err) return ZDL_EINVAL;
   if (!c->sub.empty()) return group_export(c, dev_call, dev_err);
+  if (c->sparse) return fail(c, ZDL_EINVAL, "zdl_table_export: a sparse context has no S x S table");
   HIP_TRY(c, enter(c));
   if (c->comm) {  // every rank's tables, summed
     const int rc = comm_sum_tables(c);
@@ -2312,6 +2509,7 @@ int zdl_table_import(zdl_ctx* c, const void* dev_call, const void* dev_err) {
     return group_first(c, zdl_table_import(c->sub[0], dev_call, dev_err));
   }
   if (c->ord) return fail(c, ZDL_EINVAL, "zdl_table_import: the table carries no insertion-order ranks");
+  if (c->sparse) return fail(c, ZDL_EINVAL, "zdl_table_import: a sparse context has no S x S table");
   HIP_TRY(c, enter(c));
   const size_t bytes = (size_t)c->rows * c->S * 8;
   HIP_TRY(c, hipMemcpyAsync(c->call.p, dev_call, bytes, hipMemcpyDeviceToDevice, c->stream));
@@ -2376,6 +2574,7 @@ static zdl_ctx* create_group(const zdl_config* cfg) {
     one.device = cfg->device_ids[d];
     one.n_devices = 0;
     one.device_ids = nullptr;
+    one.flags |= ZDL_FLAG_DENSE_TABLE;  // the RCCL reduce sums S x S tables
     zdl_ctx* s = zdl_create(&one);
     if (!s) {
       const std::string e = g_create_error;
@@ -2530,6 +2729,7 @@ int zdl_comm_init(zdl_ctx* c, const uint8_t* id, int rank, int world) {
   if (!c || !id || world < 1 || rank < 0 || rank >= world) return fail(c, ZDL_EINVAL, "zdl_comm_init: bad rank / world");
   if (!c->sub.empty()) return fail(c, ZDL_EINVAL, "zdl_comm_init: a device group has its own communicator");
   if (c->ord || c->days) return fail(c, ZDL_EINVAL, "zdl_comm_init: insertion order and daily buckets are per process");
+  if (c->sparse) return fail(c, ZDL_EINVAL, "zdl_comm_init: create the context with ZDL_FLAG_DENSE_TABLE (RCCL sums S x S tables)");
   if (c->comm) return fail(c, ZDL_EINVAL, "zdl_comm_init: already joined");
   HIP_TRY(c, enter(c));
   ncclUniqueId u;

@@ -52,6 +52,11 @@ hipError_t compact_links(LinkWork& w, const unsigned long long* call, const unsi
 // compact_select selects the non-zero cells and returns their number (one stream sync);
 // compact_records writes the m records (the output may be mapped pinned host memory).
 hipError_t compact_select(LinkWork& w, const unsigned long long* call, uint64_t SS, uint64_t* n_out, hipStream_t s);
+// A sparse context's sorted (cell, call, err) list as link records (zdl_sparse.h), in rank
+// order when a rank table is given.
+hipError_t compact_sparse(LinkWork& w, const uint32_t* cell, const unsigned long long* call,
+                          const unsigned long long* err, uint64_t m, uint32_t S, const int32_t* rank, uint32_t nrank,
+                          int32_t* parent, int32_t* child, int64_t* call_out, int64_t* err_out, hipStream_t s);
 hipError_t compact_records(LinkWork& w, const unsigned long long* call, const unsigned long long* err, uint64_t m,
                            uint32_t S, const int32_t* rank, uint32_t nrank, int32_t* parent, int32_t* child,
                            int64_t* call_out, int64_t* err_out, hipStream_t s);

@@ -207,6 +207,67 @@ hipError_t compact_records(LinkWork& w, const unsigned long long* call, const un
   return hipGetLastError();
 }
 
+namespace {
+__global__ void k_sparse_keys(const uint32_t* __restrict__ cell, uint64_t m, uint32_t S,
+                              const int32_t* __restrict__ rank, uint32_t nrank, uint32_t* __restrict__ keys,
+                              uint32_t* __restrict__ idx) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  const uint32_t i = cell[j];
+  keys[j] = (rank16((int32_t)(i / S), rank, nrank) << 16) | rank16((int32_t)(i % S), rank, nrank);
+  idx[j] = (uint32_t)j;
+}
+
+__global__ void k_sparse_records(const uint32_t* __restrict__ sel, uint64_t m, uint32_t S,
+                                 const uint32_t* __restrict__ cell, const unsigned long long* __restrict__ call,
+                                 const unsigned long long* __restrict__ err, int32_t* __restrict__ p,
+                                 int32_t* __restrict__ c, int64_t* __restrict__ n, int64_t* __restrict__ e) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  const uint32_t k = sel ? sel[j] : (uint32_t)j;
+  const uint32_t i = cell[k];
+  p[j] = (int32_t)(i / S);
+  c[j] = (int32_t)(i % S);
+  n[j] = (int64_t)call[k];
+  e[j] = (int64_t)err[k];
+}
+}  // namespace
+
+hipError_t compact_sparse(LinkWork& w, const uint32_t* cell, const unsigned long long* call,
+                          const unsigned long long* err, uint64_t m, uint32_t S, const int32_t* rank, uint32_t nrank,
+                          int32_t* parent, int32_t* child, int64_t* call_out, int64_t* err_out, hipStream_t s) {
+  if (m == 0) return hipSuccess;
+  if (m >= (1ull << 31)) return hipErrorInvalidValue;
+  const uint32_t* sel = nullptr;
+  if (rank) {  // the list is in cell (id) order; names order: a stable sort by the ranks
+    if (m > w.cap) {
+      for (int b = 0; b < 2; ++b) {
+        GTRY(grow(w.sel[b], m));
+        GTRY(grow(w.keys[b], m));
+      }
+      w.cap = m;
+      size_t need = 0;
+      GTRY(hipcub::DeviceRadixSort::SortPairs(nullptr, need, w.keys[0], w.keys[1], w.sel[0], w.sel[1], (int)m, 0, 32,
+                                              s));
+      if (need > w.tmp_bytes) {
+        if (w.tmp) (void)hipFree(w.tmp);
+        w.tmp = nullptr;
+        w.tmp_bytes = 0;
+        GTRY(hipMalloc(&w.tmp, need));
+        w.tmp_bytes = need;
+      }
+    }
+    hipLaunchKernelGGL(k_sparse_keys, blocks(m), dim3(256), 0, s, cell, m, S, rank, nrank, w.keys[0], w.sel[0]);
+    GTRY(hipGetLastError());
+    size_t bytes = w.tmp_bytes;
+    GTRY(hipcub::DeviceRadixSort::SortPairs(w.tmp, bytes, w.keys[0], w.keys[1], w.sel[0], w.sel[1], (int)m, 0, 32, s));
+    sel = w.sel[1];
+  }
+  hipLaunchKernelGGL(k_sparse_records, blocks(m), dim3(256), 0, s, sel, m, S, cell, call, err, parent, child,
+                     call_out, err_out);
+  return hipGetLastError();
+}
+
 hipError_t compact_links(LinkWork& w, const unsigned long long* call, const unsigned long long* err, uint64_t SS,
                          uint32_t S, const int32_t* rank, uint32_t nrank, int32_t* parent, int32_t* child,
                          int64_t* call_out, int64_t* err_out, uint64_t* n_out, hipStream_t s) {
