@@ -1,9 +1,11 @@
 """Benchmark: spans/sec linked to DependencyLinks on MI355X (BASELINE.json metric).
 
 One step = one pass of the hot path over one batch already resident in HBM:
-reset the S x S counts, zdl_put_spans_device (k_link, k_link_full, k_big), for N > 1
-one RCCL all-reduce of the count tables, then zdl_link (ordered compaction into mapped
-pinned memory, one sync) -> the DependencyLink list.
+reset the S x S counts, zdl_put_spans_device (k_link, k_tail), for N > 1 one RCCL
+all-reduce of the count tables, then zdl_link (ordered compaction into mapped pinned
+memory, one sync) -> the DependencyLink list. At N = 1 two steps are in flight (two
+contexts, two streams: step k+1 is launched before step k's links are read, so host work
+overlaps device work); `config.ms_per_step_serial` is the same step run one at a time.
 
 N = 1 runs C2 (10M spans / 1M traces / 50 services), BASELINE.json configs[1]. N > 1 is
 weak scaling on C3's shape (500 services): every rank links its own C3 per-GPU shard
@@ -216,6 +218,8 @@ def main():
     ap.add_argument("--no-h2d", action="store_true", help="skip the host-buffer (PCIe-inclusive) leg")
     ap.add_argument("--no-proto3", action="store_true", help="skip the proto3 ingest side leg")
     ap.add_argument("--no-mysql-rows", action="store_true", help="skip the mysql-v1 rows side leg")
+    ap.add_argument("--inflight", type=int, default=0,
+                    help="steps in flight (contexts used round-robin): default 2 at N = 1, 1 at N > 1")
     ap.add_argument("--no-insertion-order", action="store_true",
                     help="skip the side measurement of the insertion-order mode (N = 1 only)")
     args = ap.parse_args()
@@ -275,37 +279,66 @@ def main():
             combine = "torch.distributed all-reduce of exported tables"
     tcall = torch.zeros(S * S, dtype=torch.int64, device=dev) if combine.startswith("torch") else None
     terr = torch.zeros(S * S, dtype=torch.int64, device=dev) if combine.startswith("torch") else None
+    # Steps in flight: with 2, step k+1's reset and put (another context, its own stream) are
+    # enqueued before step k's links are read, so the host's work of reading one step's links
+    # and launching the next overlaps the GPU's work instead of idling it (~25 us a step at C2).
+    # Every step still resets, links every span and reads every link back.
+    inflight = args.inflight or (2 if world == 1 else 1)
+    ctxs = [ctx] + [N.Context(S, device=local, timing=True, timing_stride=8) for _ in range(inflight - 1)]
 
-    def step():
-        ctx.reset()
-        ctx.put_spans_device(ptrs, cols.n_spans, doff.data_ptr(), cols.n_traces)
+    def launch(c):
+        c.reset()
+        c.put_spans_device(ptrs, cols.n_spans, doff.data_ptr(), cols.n_traces)
         if tcall is not None:
-            ctx.table_export(tcall.data_ptr(), terr.data_ptr())
-            ctx.sync()
+            c.table_export(tcall.data_ptr(), terr.data_ptr())
+            c.sync()
             dist.all_reduce(tcall)
             dist.all_reduce(terr)
             torch.cuda.synchronize(dev)
-            ctx.table_import(tcall.data_ptr(), terr.data_ptr())
-        return ctx.link()
+            c.table_import(tcall.data_ptr(), terr.data_ptr())
 
-    for _ in range(args.warmup):
-        step()
-    ctx.kernel_times()  # drops the warmup puts from the k_link event ring
+    def run(k_steps):
+        """k_steps steps: every step's put is launched, every step's links are read."""
+        res = None
+        for k in range(k_steps):
+            launch(ctxs[k % inflight])
+            if k >= inflight - 1:
+                res = ctxs[(k - inflight + 1) % inflight].link()
+        for k in range(max(k_steps - inflight + 1, 0), k_steps):
+            res = ctxs[k % inflight].link()
+        return res
+
+    def sync_all():
+        for c in ctxs:
+            c.sync()
+        torch.cuda.synchronize(dev)
+
+    run(args.warmup)
+    for c in ctxs:
+        c.kernel_times()  # drops the warmup puts from the k_link event rings
     if dist:
         dist.barrier()
-    torch.cuda.synchronize(dev)
-    ctx.sync()
+    sync_all()
     t_start = time.perf_counter()
-    for _ in range(args.steps):
-        out = step()
-    ctx.sync()
-    torch.cuda.synchronize(dev)
+    out = run(args.steps)
+    sync_all()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
-    # HIP events around every timed put's k_link (a ring in the context), averaged once here
-    kt = ctx.kernel_times()
-    tiles = float(kt.tiles_ms)
+    # HIP events around every timed put's k_link (a ring per context), averaged once here
+    kts = [float(c.kernel_times().tiles_ms) for c in ctxs]
+    kts = [x for x in kts if x > 0] or [float("nan")]
+    tiles = float(np.mean(kts))
+    serial_ms = None
+    if inflight > 1:  # the same steps one at a time (reported beside `value`, not as it)
+        ns = min(args.steps, 10)
+        sync_all()
+        t1 = time.perf_counter()
+        for _ in range(ns):
+            launch(ctx)
+            ctx.link()
+        sync_all()
+        serial_ms = (time.perf_counter() - t1) / ns * 1e3
     if dist:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -420,6 +453,7 @@ def main():
             "data": "synthetic",
             "config": {"workload": w.name, "spans_per_gpu": cols.n_spans, "traces_per_gpu": cols.n_traces,
                        "services": S, "parallelism": f"trace-shard x{world}", "combine": combine,
+                       "inflight": inflight, "ms_per_step_serial": serial_ms,
                        "kernel_ms": {"k_link": tiles},
                        "step_roofline_frac": bytes_launch / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
                        "k_link_read_frac": read_launch / (tiles * 1e-3) / 1e9 / HBM_PEAK_GBS,
@@ -432,7 +466,8 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
-    ctx.close()
+    for c in ctxs:
+        c.close()
     if dist:
         dist.destroy_process_group()
 

@@ -327,3 +327,35 @@ def test_sparse_vs_dense_table_large_dictionary():
     for a, b, x, y in ((3, 4, 6, 1), (1999, 0, 2, 2)):
         x0, y0 = d.get((a, b), (0, 0))
         assert (a, b, x0 + x, y0 + y) in added
+
+
+@pytest.mark.parametrize("sparse", [False, True])
+@pytest.mark.parametrize("wave", [True, False])
+def test_mid_size_messy_traces_vs_cpp(sparse, wave, monkeypatch):
+    """Traces of 65..400 spans with C4's faults (split spans, duplicate ids, missing brokers,
+    extra roots): k_tail's wave_big (<= 208 spans, one wave each; a trace whose ids are not
+    simple is retried on the exact path by the last workgroup) and the workgroup paths
+    (ZDL_WAVE_BIG=0), dense and sparse tables, with and without a time window."""
+    if sparse:
+        monkeypatch.setenv("ZDL_SPARSE", "1")
+    if not wave:
+        monkeypatch.setenv("ZDL_WAVE_BIG", "0")
+    w = synth.Workload("mid_messy", 0x5EED0078, 80_000, 50, n_brokers=4, max_depth=16, size_dist=1,
+                       pareto_alpha=0.7, max_size=400, max_fanout=40, p_error=0.05, p_messaging=0.3,
+                       p_missing_broker=0.1, p_delete=0.05, p_extra_root=0.03, p_uninstrumented=0.1,
+                       p_drop_shared_parent=0.1, p_split=0.05)
+    cols = synth.generate(w)
+    sizes = np.diff(cols.offsets.astype(np.int64))
+    assert ((sizes > 64) & (sizes <= 208)).sum() > 1000 and (sizes > 208).sum() > 100
+    base_ms = w.base_ts_us // 1000
+    ctx = N.Context(w.total_services)
+    ctx.put_spans(cols)
+    got = sorted(_tuples(*ctx.link()))
+    ctx.reset()
+    ctx.set_window(base_ms + 60_000, 30_000)  # traces start 1 ms apart: about the middle third
+    ctx.put_spans(cols)
+    windowed = sorted(_tuples(*ctx.link()))
+    ctx.close()
+    assert got == sorted(_oracle(cols))
+    st, p, c, n, e = ref.link(cols, window=(base_ms + 60_000, 30_000), threads=16)
+    assert st == 0 and len(p) > 100 and windowed == sorted(_tuples(p, c, n, e))

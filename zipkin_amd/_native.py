@@ -9,7 +9,7 @@ from typing import Optional
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libzdl.so")
+LIB_PATH = os.environ.get("ZDL_LIB_PATH") or os.path.join(HERE, "libzdl.so")  # override: A/B builds
 
 ZDL_OK, ZDL_EINVAL, ZDL_ENOMEM, ZDL_EDEVICE, ZDL_EREF_NPE, ZDL_EREF_IAE = 0, -1, -2, -3, -4, -5
 ZDL_DICT_SERVICE, ZDL_DICT_IPV4, ZDL_DICT_IPV6 = 0, 1, 2

@@ -88,11 +88,9 @@ struct Args {
   uint32_t* big_list;   // k_link -> k_tail: the traces longer than WSMALL
   uint32_t* big_count;
   uint32_t* status;
-  uint32_t small_max;    // traces longer than this are k_tail's (big_traces)
+  uint32_t small_max;    // traces longer than this are k_tail's (big_one, wave_big)
   uint32_t* cx_count;
-  uint32_t* cx_count_next;   // the next put's counters (two slots alternate by put):
-  uint32_t* big_count_next;  // zeroed by this put's k_tail, so no memset is needed
-  unsigned long long* map;   // mapped pinned host buffer: k_tail's last workgroup writes the
+  unsigned long long* map;  // mapped pinned host buffer: k_tail's last workgroup writes the
                              // ordered link records there (S*S <= 8192), else nullptr
   uint32_t* done;            // k_tail workgroups finished (the last one compacts; resets it)
   unsigned long long* flag;  // mapped pinned: k_tail's last workgroup stores `seq` after the
@@ -151,7 +149,22 @@ struct Args {
   uint32_t* tlg;
   uint32_t* tseg_big;
   uint32_t* tseg_win;
+  // k_tail's big traces: k_link lists those of at most wb_max spans (wave_big: one wave each)
+  // from the front of big_list (big_count), the others from its back (big_list[big_cap - 1 - j],
+  // large_count: one workgroup each); k_tail takes them by tickets, the workgroup ones first.
+  // A wave_big trace that is not simple is retried by k_tail's last workgroup (retry list).
+  uint32_t wb_max;
+  uint32_t big_cap;
+  uint32_t* large_count;
+  uint32_t* tick_large;
+  uint32_t* tick_mid;
+  uint32_t* retry_count;
+  uint32_t* retry;
+  uint32_t* ctr_next;  // the next put's counter block, zeroed by this put's k_tail (CTR_* slots)
 };
+// The counter block of one put (two alternate by put, so no put issues a memset)
+enum : int { CTR_MID = 0, CTR_CX = 1, CTR_LARGE = 2, CTR_TICK_LARGE = 3, CTR_TICK_MID = 4, CTR_RETRY = 5, CTR_N = 8 };
+constexpr int CTR_DONE = 2 * CTR_N;  // k_tail's finished-workgroup count (after both blocks)
 
 #include "zdl_full.inc"  // the full per-window emulation (k_tail's first part)
 #include "zdl_link.inc"  // k_link, full_windows (need zdl_full.inc's helpers)
@@ -333,7 +346,7 @@ __device__ __forceinline__ int bs_find(const BSView& v, uint64_t key, int n) {
   }
 }
 
-__device__ bool big_simple(const Args& A, unsigned char* lds, size_t lds_bytes, uint64_t b, int n, uint32_t day,
+__device__ __forceinline__ bool big_simple(const Args& A, unsigned char* lds, size_t lds_bytes, uint64_t b, int n, uint32_t day,
                            uint32_t* scnt) {
   __shared__ int sh_bad, sh_more;
   __shared__ unsigned long long sh_rootid;
@@ -518,52 +531,457 @@ __device__ bool big_simple(const Args& A, unsigned char* lds, size_t lds_bytes, 
   return true;
 }
 
+// ---------------------------------------------------------------- wave_big
+// Traces of WSMALL < n <= WB_MAX spans with simple ids, one wave each: big_simple's algorithm
+// at wave scale (wave_sync instead of workgroup barriers), so a CU links 16 such traces at
+// once instead of one. Lane l owns spans l, l + 64, ... (at most WB_K). The wave's LDS carve
+// holds id, parent id, services, local endpoint and flags, the id hash (2 slots per span: u32
+// words of non-shared | shared span index + 1, keys compared through the id array), the
+// pointer-jumping arrays (i16) and has-children bytes: 49 B per span.
+constexpr int WB_CARVE = 9600;              // bytes per wave (16 waves: 150 KB of k_tail's LDS)
+constexpr int WB_SCR = WB_CARVE - 32;       // 4 u64 scratch words: root id, window index / min, count
+constexpr int WB_MAX = 192;
+constexpr int WB_K = (WB_MAX + 63) / 64;
+static_assert(49 * WB_MAX <= WB_SCR && WB_MAX % 8 == 0 && WB_MAX < 32767, "wave_big carve");
+struct WBv {
+  uint64_t* id;
+  uint64_t* pid;
+  int32_t* ls;
+  int32_t* rs;
+  int32_t* i4;
+  int32_t* i6;
+  uint32_t* pf;
+  uint32_t* slot;
+  int16_t* a;
+  int16_t* nm;
+  uint8_t* hasc;
+};
+__device__ __forceinline__ WBv wb_view(unsigned char* p, int n) {
+  const int m = (n + 7) & ~7;
+  WBv v;
+  v.id = reinterpret_cast<uint64_t*>(p);
+  v.pid = v.id + m;
+  v.ls = reinterpret_cast<int32_t*>(v.pid + m);
+  v.rs = v.ls + m;
+  v.i4 = v.rs + m;
+  v.i6 = v.i4 + m;
+  v.pf = reinterpret_cast<uint32_t*>(v.i6 + m);
+  v.slot = v.pf + m;
+  v.a = reinterpret_cast<int16_t*>(v.slot + 2 * m);
+  v.nm = v.a + m;
+  v.hasc = reinterpret_cast<uint8_t*>(v.nm + m);
+  return v;
+}
+__device__ __forceinline__ int wb_home(uint64_t key, int H) {
+  const uint32_t h = ((uint32_t)key ^ (uint32_t)(key >> 32)) * 0x9E3779B1u;
+  return (int)__umulhi(h, (uint32_t)H);
+}
+__device__ __forceinline__ uint32_t wb_word_idx(uint32_t w) { return ((w & 0xFFFFu) ? (w & 0xFFFFu) : (w >> 16)) - 1u; }
+// The slot word of key (0 if absent)
+__device__ __forceinline__ uint32_t wb_find(const WBv& v, uint64_t key, int H) {
+  int q = wb_home(key, H);
+  while (true) {
+    const uint32_t w = v.slot[q];
+    if (w == 0u || v.id[wb_word_idx(w)] == key) return w;
+    q = q + 1 == H ? 0 : q + 1;
+  }
+}
+
+// Links trace big_list[bi] (n <= WB_MAX spans) with the calling wave (every lane calls).
+// Returns false when its ids are not simple: nothing was counted, the caller retries it on the
+// exact path. A bad service id fails the put like big_simple; a trace outside the time window
+// counts nothing (big_one's rule: its first parentless timestamp, else its minimum).
+__device__ __forceinline__ bool wave_big(const Args& A, unsigned char* p, uint32_t bi, int lane) {
+  const uint32_t t = A.big_list[bi];
+  const uint64_t b = A.off[t], e = A.off[t + 1];
+  if (e < b || e > A.n_spans || e - b > (uint64_t)WB_MAX) {  // k_link flagged it
+    if (A.sparse && lane == 0) A.tseg_big[bi] = 0;
+    return true;
+  }
+  const int n = (int)(e - b), H = 2 * ((n + 7) & ~7);
+  const WBv v = wb_view(p, n);
+  unsigned long long* scr = reinterpret_cast<unsigned long long*>(p + WB_SCR);
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(scr + 3);
+  if (lane < 3) scr[lane] = ~0ull;
+  if (lane == 3) scr[3] = 0ull;
+  for (int q = lane; q < H; q += 64) v.slot[q] = 0u;
+  bool bad = false;
+  // the spans into the carve (every column's loads first: one round trip for the trace)
+  uint64_t id[WB_K], pid[WB_K];
+  int32_t ls[WB_K], rs[WB_K], i4[WB_K], i6[WB_K];
+  uint32_t pf[WB_K];
+#pragma unroll
+  for (int k = 0; k < WB_K; ++k) {
+    const int i = lane + 64 * k;
+    if (i >= n) continue;
+    const uint64_t g = b + i;
+    id[k] = A.c.id[g];
+    pid[k] = A.c.pid[g];
+    ls[k] = A.c.lsvc[g];
+    rs[k] = A.c.rsvc[g];
+    i4[k] = A.c.ip4[g];
+    i6[k] = A.c.ip6[g];
+    pf[k] = A.c.pf[g];
+  }
+#pragma unroll
+  for (int k = 0; k < WB_K; ++k) {
+    const int i = lane + 64 * k;
+    if (i >= n) continue;
+    v.id[i] = id[k];
+    v.pid[i] = pid[k] == id[k] ? 0 : pid[k];  // Span.build drops a self parent (Span.java:611-617)
+    v.ls[i] = ls[k];
+    v.rs[i] = rs[k];
+    v.i4[i] = i4[k];
+    v.i6[i] = i6[k];
+    v.pf[i] = pf[k];
+    v.hasc[i] = 0;
+    bad |= ((uint32_t)ls[k] >= A.S && ls[k] >= 0) || ((uint32_t)rs[k] >= A.S && rs[k] >= 0);
+  }
+  wave_sync();
+  if (A.window) {
+#pragma unroll
+    for (int k = 0; k < WB_K; ++k) {
+      const int i = lane + 64 * k;
+      if (i >= n) continue;
+      const int64_t x = A.c.ts[b + i];
+      if (x == 0) continue;
+      if (v.pid[i] == 0) atomicMin(&scr[1], (unsigned long long)i);
+      atomicMin(&scr[2], (unsigned long long)x);
+    }
+    wave_sync();
+    const unsigned long long fi = scr[1], mn = scr[2];
+    const int64_t ts = fi != ~0ull ? A.c.ts[b + fi] : (mn == ~0ull ? 0 : (int64_t)mn);
+    if (!window_pass(ts, A.win_lo, A.win_hi)) {
+      if (A.sparse && lane == 0) A.tseg_big[bi] = 0;
+      return true;
+    }
+  }
+  if (ballot(bad)) {  // counted nowhere: the put fails
+    if (lane == 0) {
+      atomicOr(A.status, ST_BADSVC);
+      if (A.sparse) A.tseg_big[bi] = 0;
+    }
+    return true;
+  }
+  // 1. the id hash; a second span with one (id, shared) -> not simple
+  bool dup = false;
+#pragma unroll
+  for (int k = 0; k < WB_K; ++k) {
+    const int i = lane + 64 * k;
+    if (i >= n) continue;
+    const uint64_t my = v.id[i];
+    const bool sh = is_shared(v.pf[i]);
+    const uint32_t mine = sh ? (uint32_t)(i + 1) << 16 : (uint32_t)(i + 1);
+    int q = wb_home(my, H);
+    while (true) {
+      uint32_t w = v.slot[q];
+      if (w == 0u) {
+        w = atomicCAS(&v.slot[q], 0u, mine);
+        if (w == 0u) break;
+      }
+      if (v.id[wb_word_idx(w)] == my) {
+        dup |= (atomicOr(&v.slot[q], mine) & (sh ? 0xFFFF0000u : 0xFFFFu)) != 0u;
+        break;
+      }
+      q = q + 1 == H ? 0 : q + 1;
+    }
+    if (!sh && v.pid[i] == 0) atomicMin(&scr[0], (unsigned long long)my);
+  }
+  wave_sync();
+  if (ballot(dup)) return false;
+  const unsigned long long rootid = scr[0];
+  const int rp = rootid != ~0ull ? (int)(wb_find(v, rootid, H) & 0xFFFFu) - 1 : -1;
+  const int root_attach = rp >= 0 ? rp : PAR_TERMINAL;
+  // 2. tree parents (+ the shared spans' parent-id backfill, Trace.java:76-79: only shared
+  // spans' entries change, and only their own lane reads them again) and has-children
+#pragma unroll
+  for (int k = 0; k < WB_K; ++k) {
+    const int i = lane + 64 * k;
+    if (i >= n) continue;
+    const uint32_t pfi = v.pf[i];
+    const uint64_t pidi = v.pid[i];
+    int par;
+    if (is_shared(pfi)) {
+      const int ns_own = (int)(wb_find(v, v.id[i], H) & 0xFFFFu) - 1;
+      par = ns_own >= 0 ? ns_own : root_attach;
+      if (ns_own >= 0 && pidi == 0) v.pid[i] = v.pid[ns_own];
+    } else if (i == rp) {
+      par = PAR_TERMINAL;
+    } else if (pidi != 0) {
+      const uint32_t w = wb_find(v, pidi, H);
+      const int nss = (int)(w & 0xFFFFu) - 1, shs = (int)(w >> 16) - 1;
+      const bool same_ep = shs >= 0 && v.ls[shs] == v.ls[i] && v.i4[shs] == v.i4[i] && v.i6[shs] == v.i6[i] &&
+                           port_of(v.pf[shs]) == port_of(pfi);
+      par = same_ep ? shs : (nss >= 0 ? nss : root_attach);
+    } else {
+      par = root_attach;
+    }
+    v.a[i] = (int16_t)par;
+    v.nm[i] = (int16_t)par;
+    if (par >= 0) v.hasc[par] = 1;
+  }
+  wave_sync();
+  // 3. pointer jumping: a -> PAR_TERMINAL iff reachable, nm -> nearest ancestor with a kind
+  int rounds = 4;
+  for (int m = n; m > 1; m >>= 1) rounds += 2;
+  for (int r = 0; r < rounds; ++r) {
+    bool more = false;
+#pragma unroll
+    for (int k = 0; k < WB_K; ++k) {
+      const int i = lane + 64 * k;
+      if (i >= n) continue;
+      const int x = v.a[i];
+      if (x >= 0) {
+        v.a[i] = v.a[x];
+        more = true;
+      }
+      const int y = v.nm[i];
+      if (y >= 0 && kind_of(v.pf[y]) == ZDL_KIND_NULL) {
+        v.nm[i] = v.nm[y];
+        more = true;
+      }
+    }
+    wave_sync();
+    if (!ballot(more)) break;
+  }
+  // 4. DependencyLinker's rules per node (DependencyLinker.java:58-148)
+  auto emit = [&](int32_t x, int32_t y, bool er) {
+    const uint32_t idx = (uint32_t)x * A.S + (uint32_t)y;
+    if (A.sparse) {  // the trace's log segment
+      A.tlg[2 * b + atomicAdd(cnt, 1u)] = (idx << 1) | (er ? 1u : 0u);
+      return;
+    }
+    atomicAdd(&A.call[idx], 1ull);
+    if (er) atomicAdd(&A.err[idx], 1ull);
+  };
+#pragma unroll
+  for (int k = 0; k < WB_K; ++k) {
+    const int i = lane + 64 * k;
+    if (i >= n || v.a[i] != PAR_TERMINAL) continue;  // unreachable: a cycle not through the root
+    const uint32_t pfi = v.pf[i];
+    const uint32_t kind0 = kind_of(pfi);
+    if (kind0 == ZDL_KIND_CLIENT && v.hasc[i]) continue;
+    const int32_t svc = v.ls[i], rsvc = v.rs[i];
+    uint32_t kind = kind0;
+    if (kind == ZDL_KIND_NULL) {
+      if (svc >= 0 && rsvc >= 0) kind = ZDL_KIND_CLIENT; else continue;
+    }
+    const bool srv = kind == ZDL_KIND_SERVER || kind == ZDL_KIND_CONSUMER;
+    int32_t pa = srv ? rsvc : svc;
+    const int32_t ch = srv ? svc : rsvc;
+    if (srv && i == rp && pa < 0) continue;
+    bool er = err_of(pfi);
+    if (kind == ZDL_KIND_PRODUCER || kind == ZDL_KIND_CONSUMER) {
+      if (pa >= 0 && ch >= 0) emit(pa, ch, er);
+      continue;
+    }
+    const int ra = v.nm[i];
+    if (ra >= 0) {
+      const int32_t ran = v.ls[ra];
+      if (ran >= 0) {
+        if (kind == ZDL_KIND_CLIENT && svc >= 0 && ran != svc) emit(ran, svc, false);
+        if (kind == ZDL_KIND_SERVER || pa < 0) pa = ran;
+        const uint32_t apf = v.pf[ra];
+        const uint64_t pidi = v.pid[i];
+        if (!er && kind_of(apf) == ZDL_KIND_CLIENT && pidi != 0 && pidi == v.id[ra]) er = err_of(apf);
+      }
+    }
+    if (pa >= 0 && ch >= 0) emit(pa, ch, er);
+  }
+  wave_sync();
+  if (A.sparse && lane == 0) A.tseg_big[bi] = *cnt;
+  return true;
+}
+
+// k_mid, between k_link and k_tail: every wave takes front-list traces by ticket, WB_CHUNK per
+// ticket (the next ticket fetched while the current ones are linked); a trace that is not
+// simple goes to the retry list, which k_tail's workgroups take after the back list. A
+// kernel of its own: wave_big's registers then never meet k_tail's (one kernel spilled both).
+constexpr uint32_t WB_CHUNK = 8;
+constexpr int MID_WG = 256;  // 4 waves: 4 workgroups (16 carves, 150 KB of LDS) per CU
+__global__ void __launch_bounds__(MID_WG) k_mid(Args A) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  unsigned char* p = lds + (size_t)w * WB_CARVE;
+  const uint32_t nmid = *A.big_count;
+  if (nmid == 0) return;  // no ticket traffic when there is nothing (every wave on one address)
+  uint32_t c = 0;
+  if (lane == 0) c = atomicAdd(A.tick_mid, 1u);
+  c = __builtin_amdgcn_readfirstlane(c);
+  while (c * WB_CHUNK < nmid) {
+    uint32_t nx = 0;
+    if (lane == 0) nx = atomicAdd(A.tick_mid, 1u);
+    const uint32_t j1 = min(nmid, (c + 1) * WB_CHUNK);
+    for (uint32_t j = c * WB_CHUNK; j < j1; ++j) {
+      if (!wave_big(A, p, j, lane) && lane == 0)
+        __hip_atomic_store(&A.retry[atomicAdd(A.retry_count, 1u)], j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      wave_sync();  // the carve is reused
+    }
+    c = __builtin_amdgcn_readfirstlane(nx);
+  }
+}
+
+// The exact path for one big trace (every thread of the workgroup calls): the spans copied to
+// HBM scratch at the trace's offset, bitonic-sorted by Trace.merge's comparator, merged,
+// the SpanNode tree and DependencyLinker's rules (zdl_algo.h). Runs for non-simple traces
+// (and every big trace in insertion order) only.
 template <int ORD>
-__device__ __forceinline__ void big_traces(const Args& A, unsigned char* lds, size_t lds_bytes) {
-  __shared__ uint32_t sh_cnt;  // sparse: links logged for the current trace
+__device__ __forceinline__ void big_exact(const Args& A, uint64_t b, int n, uint32_t day, uint32_t bi) {
+  __shared__ uint32_t sh_cnt;  // sparse: links logged for the trace
   __shared__ int32_t sh_root;
+  View v;
+  v.id = A.b_id + b;
+  v.pid = A.b_pid + b;
+  v.lsvc = A.b_lsvc + b;
+  v.rsvc = A.b_rsvc + b;
+  v.ip4 = A.b_ip4 + b;
+  v.ip6 = A.b_ip6 + b;
+  v.pf = A.b_pf + b;
+  v.perm = A.b_perm + b;
+  v.parent = A.b_parent + b;
+  v.live = A.b_live + b;
+  v.haschild = A.b_haschild + b;
+  if (threadIdx.x == 0) {
+    sh_cnt = 0;
+    sh_root = 0x7fffffff;
+  }
+  for (int s = threadIdx.x; s < n; s += BIG_WG) {
+    const uint64_t g = b + s;
+    const uint64_t id = A.c.id[g];
+    uint64_t pid = A.c.pid[g];
+    if (pid == id) pid = 0;  // Span.build drops a self parent (Span.java:611-617)
+    v.id[s] = id;
+    v.pid[s] = pid;
+    v.lsvc[s] = A.c.lsvc[g];
+    v.rsvc[s] = A.c.rsvc[g];
+    v.ip4[s] = A.c.ip4[g];
+    v.ip6[s] = A.c.ip6[g];
+    v.pf[s] = A.c.pf[g];
+    v.perm[s] = s;
+    v.haschild[s] = 0;
+  }
+  big_sync();
+  // bitonic sort of perm by span_less (any n: out-of-range partners are +inf)
+  int npad = 1;
+  while (npad < n) npad <<= 1;
+  for (int kk = 2; kk <= npad; kk <<= 1) {
+    for (int i = threadIdx.x; i < n; i += BIG_WG) {
+      const int l = i ^ (kk - 1);
+      if (l > i && l < n) {
+        const uint32_t a = v.perm[i], c = v.perm[l];
+        if (span_less(v, A.R, c, a)) { v.perm[i] = c; v.perm[l] = a; }
+      }
+    }
+    big_sync();
+    for (int jj = kk >> 2; jj > 0; jj >>= 1) {
+      for (int i = threadIdx.x; i < n; i += BIG_WG) {
+        const int l = i ^ jj;
+        if (l > i && l < n) {
+          const uint32_t a = v.perm[i], c = v.perm[l];
+          if (span_less(v, A.R, c, a)) { v.perm[i] = c; v.perm[l] = a; }
+        }
+      }
+      big_sync();
+    }
+  }
+  bool npe = false;
+  for (int p = threadIdx.x; p < n; p += BIG_WG) {
+    const uint64_t my = v.id[v.perm[p]];
+    if (p != 0 && v.id[v.perm[p - 1]] == my) continue;
+    int ge = p + 1;
+    while (ge < n && v.id[v.perm[ge]] == my) ++ge;
+    if (ge == p + 1) { v.live[p] = 1; continue; }
+    npe |= merge_group(v, p, ge);
+  }
+  if (npe) atomicOr(A.status, ST_NPE);
+  big_sync();
+  for (int p = threadIdx.x; p < n; p += BIG_WG) {
+    const uint32_t s = v.perm[p];
+    if (v.live[p] && !is_shared(v.pf[s]) && v.pid[s] == 0) atomicMin(&sh_root, p);
+  }
+  big_sync();
+  const int rp = sh_root == 0x7fffffff ? -1 : sh_root;
+  for (int p = threadIdx.x; p < n; p += BIG_WG) {
+    const uint64_t my = v.id[v.perm[p]];
+    if (p != 0 && v.id[v.perm[p - 1]] == my) continue;
+    int ge = p + 1;
+    while (ge < n && v.id[v.perm[ge]] == my) ++ge;
+    resolve_group(v, 0, n, p, ge, rp);
+  }
+  big_sync();
+  for (int p = threadIdx.x; p < n; p += BIG_WG) {
+    const int32_t q = v.parent[p];
+    if (q >= 0) v.haschild[q] = 1;
+  }
+  big_sync();
+  uint32_t* bfs = nullptr;
+  if (ORD) {
+    if (n >= (1 << 21) - 1) {  // ranks pack positions in 21 bits
+      if (threadIdx.x == 0) atomicOr(A.status, ST_ORDLIM);
+      big_sync();
+      return;
+    }
+    bfs = A.o_bfs + b;
+    big_bfs(v, n, rp, A.o_key + b, A.o_fa + b, A.o_fb + b, bfs);
+    big_sync();
+  }
+  if (ORD && A.tr_parent) {  // ZDL_FLAG_TREE_EXPORT (wave_tree_export's encoding)
+    for (int p = threadIdx.x; p < n; p += BIG_WG) {
+      int head = p;
+      while (!v.live[head] && head > 0 && v.id[v.perm[head - 1]] == v.id[v.perm[p]]) --head;
+      const uint64_t slot = b + v.perm[p];
+      A.tr_node[slot] = (int32_t)(b + v.perm[head]);
+      const int par = v.parent[p];
+      int32_t pr = -3, bf = -1;
+      if (v.live[p] && par != PAR_NONMEMBER) {
+        pr = p == rp ? -2 : (par == PAR_TERMINAL ? -1 : (int32_t)(b + v.perm[par]));
+        int q = par, steps = 0;
+        while (q >= 0 && steps++ <= n) q = v.parent[q];
+        if (q == PAR_TERMINAL) bf = (int32_t)bfs[p];
+      }
+      A.tr_parent[slot] = pr;
+      A.tr_bfs[slot] = bf;
+    }
+  }
+  for (int p = threadIdx.x; p < n; p += BIG_WG) {
+    if (v.parent[p] == PAR_NONMEMBER) continue;
+    link_node(v, p, rp, n, [&](int32_t a, int32_t c, bool e, int k) {
+      if ((uint32_t)a >= A.S || (uint32_t)c >= A.S) { atomicOr(A.status, ST_BADSVC); return; }
+      const size_t idx = ((size_t)day * A.S + (size_t)a) * A.S + c;  // row day * S + parent
+      if (A.sparse) {
+        A.tlg[2 * b + atomicAdd(&sh_cnt, 1u)] = ((uint32_t)idx << 1) | (e ? 1u : 0u);
+        return;
+      }
+      atomicAdd(&A.call[idx], 1ull);
+      if (e) atomicAdd(&A.err[idx], 1ull);
+      if (ORD) ord_min(&A.first[idx], ord_rank(A.span_base + b, bfs[p], k));
+    });
+  }
+  big_sync();
+  if (A.sparse && threadIdx.x == 0) A.tseg_big[bi] = sh_cnt;
+}
+
+// One big trace with the workgroup (every thread calls): the time-window / day filters, then
+// big_simple, else (or with try_simple false) the exact path.
+template <int ORD>
+__device__ __forceinline__ void big_one(const Args& A, unsigned char* lds, size_t lds_bytes, uint32_t bi, bool try_simple) {
+  __shared__ uint32_t sh_cnt;  // sparse: links logged for the current trace (big_simple)
   __shared__ int sh_act;
   __shared__ int64_t sh_ts_root_idx, sh_ts_min;
-  const uint32_t nbig = *A.big_count;
-  for (uint32_t bi = blockIdx.x; bi < nbig; bi += gridDim.x) {
+  do {
     const uint32_t t = A.big_list[bi];
     const uint64_t b = A.off[t];
-    if (A.off[t + 1] < b || A.off[t + 1] > A.n_spans) continue;  // k_link flagged it
+    if (A.off[t + 1] < b || A.off[t + 1] > A.n_spans) {  // k_link flagged it
+      if (A.sparse && threadIdx.x == 0) A.tseg_big[bi] = 0;
+      break;
+    }
     const int n = (int)(A.off[t + 1] - b);
-    View v;
-    v.id = A.b_id + b;
-    v.pid = A.b_pid + b;
-    v.lsvc = A.b_lsvc + b;
-    v.rsvc = A.b_rsvc + b;
-    v.ip4 = A.b_ip4 + b;
-    v.ip6 = A.b_ip6 + b;
-    v.pf = A.b_pf + b;
-    v.perm = A.b_perm + b;
-    v.parent = A.b_parent + b;
-    v.live = A.b_live + b;
-    v.haschild = A.b_haschild + b;
     if (threadIdx.x == 0) {
       sh_cnt = 0;
       if (A.sparse) A.tseg_big[bi] = 0;  // a trace skipped below logs nothing
-      sh_root = 0x7fffffff;
       sh_act = 1;
       sh_ts_root_idx = 0x7fffffffffffffffll;
       sh_ts_min = 0;
-    }
-    for (int s = threadIdx.x; s < n; s += BIG_WG) {
-      const uint64_t g = b + s;
-      const uint64_t id = A.c.id[g];
-      uint64_t pid = A.c.pid[g];
-      if (pid == id) pid = 0;
-      v.id[s] = id;
-      v.pid[s] = pid;
-      v.lsvc[s] = A.c.lsvc[g];
-      v.rsvc[s] = A.c.rsvc[g];
-      v.ip4[s] = A.c.ip4[g];
-      v.ip6[s] = A.c.ip6[g];
-      v.pf[s] = A.c.pf[g];
-      v.perm[s] = s;
-      v.haschild[s] = 0;
     }
     big_sync();
     if (A.window) {
@@ -571,7 +989,8 @@ __device__ __forceinline__ void big_traces(const Args& A, unsigned char* lds, si
       for (int s = threadIdx.x; s < n; s += BIG_WG) {
         const int64_t x = A.c.ts[b + s];
         if (x == 0) continue;
-        if (v.pid[s] == 0) atomicMin((long long*)&sh_ts_root_idx, (long long)s);
+        const uint64_t pid = A.c.pid[b + s];
+        if (pid == 0 || pid == A.c.id[b + s]) atomicMin((long long*)&sh_ts_root_idx, (long long)s);
       }
       big_sync();
       if (threadIdx.x == 0 && sh_ts_root_idx != 0x7fffffffffffffffll)
@@ -626,109 +1045,13 @@ __device__ __forceinline__ void big_traces(const Args& A, unsigned char* lds, si
       if (sh_ts_min < 0) { big_sync(); continue; }
     }
     const uint32_t day = A.days ? (uint32_t)sh_ts_min : 0u;
-    if (!ORD && !A.skip_simple && big_simple(A, lds, lds_bytes, b, n, day, &sh_cnt)) {  // else the exact path
+    if (!ORD && try_simple && !A.skip_simple && big_simple(A, lds, lds_bytes, b, n, day, &sh_cnt)) {
       if (A.sparse && threadIdx.x == 0) A.tseg_big[bi] = sh_cnt;
       continue;
     }
-    // bitonic sort of perm by span_less (any n: out-of-range partners are +inf)
-    int npad = 1;
-    while (npad < n) npad <<= 1;
-    for (int kk = 2; kk <= npad; kk <<= 1) {
-      for (int i = threadIdx.x; i < n; i += BIG_WG) {
-        const int l = i ^ (kk - 1);
-        if (l > i && l < n) {
-          const uint32_t a = v.perm[i], c = v.perm[l];
-          if (span_less(v, A.R, c, a)) { v.perm[i] = c; v.perm[l] = a; }
-        }
-      }
-      big_sync();
-      for (int jj = kk >> 2; jj > 0; jj >>= 1) {
-        for (int i = threadIdx.x; i < n; i += BIG_WG) {
-          const int l = i ^ jj;
-          if (l > i && l < n) {
-            const uint32_t a = v.perm[i], c = v.perm[l];
-            if (span_less(v, A.R, c, a)) { v.perm[i] = c; v.perm[l] = a; }
-          }
-        }
-        big_sync();
-      }
-    }
-    bool npe = false;
-    for (int p = threadIdx.x; p < n; p += BIG_WG) {
-      const uint64_t my = v.id[v.perm[p]];
-      if (p != 0 && v.id[v.perm[p - 1]] == my) continue;
-      int ge = p + 1;
-      while (ge < n && v.id[v.perm[ge]] == my) ++ge;
-      if (ge == p + 1) { v.live[p] = 1; continue; }
-      npe |= merge_group(v, p, ge);
-    }
-    if (npe) atomicOr(A.status, ST_NPE);
-    big_sync();
-    for (int p = threadIdx.x; p < n; p += BIG_WG) {
-      const uint32_t s = v.perm[p];
-      if (v.live[p] && !is_shared(v.pf[s]) && v.pid[s] == 0) atomicMin(&sh_root, p);
-    }
-    big_sync();
-    const int rp = sh_root == 0x7fffffff ? -1 : sh_root;
-    for (int p = threadIdx.x; p < n; p += BIG_WG) {
-      const uint64_t my = v.id[v.perm[p]];
-      if (p != 0 && v.id[v.perm[p - 1]] == my) continue;
-      int ge = p + 1;
-      while (ge < n && v.id[v.perm[ge]] == my) ++ge;
-      resolve_group(v, 0, n, p, ge, rp);
-    }
-    big_sync();
-    for (int p = threadIdx.x; p < n; p += BIG_WG) {
-      const int32_t q = v.parent[p];
-      if (q >= 0) v.haschild[q] = 1;
-    }
-    big_sync();
-    uint32_t* bfs = nullptr;
-    if (ORD) {
-      if (n >= (1 << 21) - 1) {  // ranks pack positions in 21 bits
-        if (threadIdx.x == 0) atomicOr(A.status, ST_ORDLIM);
-        big_sync();
-        continue;
-      }
-      bfs = A.o_bfs + b;
-      big_bfs(v, n, rp, A.o_key + b, A.o_fa + b, A.o_fb + b, bfs);
-      big_sync();
-    }
-    if (ORD && A.tr_parent) {  // ZDL_FLAG_TREE_EXPORT (wave_tree_export's encoding)
-      for (int p = threadIdx.x; p < n; p += BIG_WG) {
-        int head = p;
-        while (!v.live[head] && head > 0 && v.id[v.perm[head - 1]] == v.id[v.perm[p]]) --head;
-        const uint64_t slot = b + v.perm[p];
-        A.tr_node[slot] = (int32_t)(b + v.perm[head]);
-        const int par = v.parent[p];
-        int32_t pr = -3, bf = -1;
-        if (v.live[p] && par != PAR_NONMEMBER) {
-          pr = p == rp ? -2 : (par == PAR_TERMINAL ? -1 : (int32_t)(b + v.perm[par]));
-          int q = par, steps = 0;
-          while (q >= 0 && steps++ <= n) q = v.parent[q];
-          if (q == PAR_TERMINAL) bf = (int32_t)bfs[p];
-        }
-        A.tr_parent[slot] = pr;
-        A.tr_bfs[slot] = bf;
-      }
-    }
-    for (int p = threadIdx.x; p < n; p += BIG_WG) {
-      if (v.parent[p] == PAR_NONMEMBER) continue;
-      link_node(v, p, rp, n, [&](int32_t a, int32_t c, bool e, int k) {
-        if ((uint32_t)a >= A.S || (uint32_t)c >= A.S) { atomicOr(A.status, ST_BADSVC); return; }
-        const size_t idx = ((size_t)day * A.S + (size_t)a) * A.S + c;  // row day * S + parent
-        if (A.sparse) {
-          A.tlg[2 * b + atomicAdd(&sh_cnt, 1u)] = ((uint32_t)idx << 1) | (e ? 1u : 0u);
-          return;
-        }
-        atomicAdd(&A.call[idx], 1ull);
-        if (e) atomicAdd(&A.err[idx], 1ull);
-        if (ORD) ord_min(&A.first[idx], ord_rank(A.span_base + b, bfs[p], k));
-      });
-    }
-    big_sync();
-    if (A.sparse && threadIdx.x == 0) A.tseg_big[bi] = sh_cnt;
-  }
+    big_exact<ORD>(A, b, n, day, bi);
+  } while (false);
+  big_sync();
 }
 
 // ---------------------------------------------------------------- k_compact
@@ -828,19 +1151,37 @@ __global__ void __launch_bounds__(COMPACT_WG) k_compact_ordered(const unsigned l
 // table into the mapped host buffer, so zdl_link needs no kernel. Also zeroes the next
 // put's counters.
 static_assert(TAIL_WG == BIG_WG && TAIL_WG == COMPACT_WG, "k_tail runs all three parts");
-constexpr size_t tail_block_bytes(int window) { return WTABLE_BYTES + (TAIL_WG / 64) * wl::bytes(window); }
+constexpr size_t tail_block_bytes(int window) {  // full_windows' table + carves; at least 150 KB (big_simple)
+  return WTABLE_BYTES + (TAIL_WG / 64) * wl::bytes(window) > (size_t)(TAIL_WG / 64) * WB_CARVE
+             ? WTABLE_BYTES + (TAIL_WG / 64) * wl::bytes(window)
+             : (size_t)(TAIL_WG / 64) * WB_CARVE;
+}
 
 template <int DENSE, int WINDOW, int ORD>
 __global__ void __launch_bounds__(TAIL_WG, 1) k_tail(Args A) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   __shared__ bool last;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    *A.cx_count_next = 0;
-    *A.big_count_next = 0;
-  }
+  if (blockIdx.x == 0 && threadIdx.x < CTR_N) A.ctr_next[threadIdx.x] = 0;
   full_windows<DENSE, WINDOW, TAIL_WG / 64, ORD>(A, lds);
   __syncthreads();
-  big_traces<ORD>(A, lds, tail_block_bytes(WINDOW));
+  // big_list's back (traces longer than wb_max), then the traces k_mid could not link (not
+  // simple), one workgroup each, by ticket (the next one fetched while this trace is linked),
+  // so that a giant trace delays only its own workgroup
+  __shared__ uint32_t sh_j;
+  const uint32_t nlarge = *A.large_count;
+  const uint32_t nbig = nlarge + (A.wb_max ? *A.retry_count : 0u);
+  if (nbig) {
+    if (threadIdx.x == 0) sh_j = atomicAdd(A.tick_large, 1u);
+    while (true) {
+      __syncthreads();
+      const uint32_t j = sh_j;
+      __syncthreads();
+      if (j >= nbig) break;
+      if (threadIdx.x == 0) sh_j = atomicAdd(A.tick_large, 1u);
+      const bool back = j < nlarge;
+      big_one<ORD>(A, lds, tail_block_bytes(WINDOW), back ? A.big_cap - 1u - j : A.retry[j - nlarge], back);
+    }
+  }
   if (!A.map) return;
   // Hand-off to the last workgroup (MI355X_MICROARCH.md, "Valid forms", first table row):
   // the table and status updates are agent-scope atomics, performed at the memory side;
@@ -982,7 +1323,8 @@ struct zdl_ctx {
   uint64_t span_base = 0;
   DevBuf<uint32_t> o_fa, o_fb, o_bfs;
   // per-put scratch
-  DevBuf<uint32_t> big_list, counters;  // counters: big[2], cx[2], alternating by put
+  DevBuf<uint32_t> big_list, counters;  // counters: two CTR_N blocks alternating by put, then done
+  DevBuf<uint32_t> retry;  // k_tail: wave_big traces for the exact path
   uint32_t epoch = 0;
   DevBuf<uint64_t> cx_win;
   // LOG mode (zdl_log.inc): the emit log, its grouped copy, per-wave segments and counts
@@ -1017,7 +1359,8 @@ struct zdl_ctx {
   DevBuf<int32_t> b_nm;
   DevBuf<unsigned long long> b_hk;
   DevBuf<uint32_t> b_hv;
-  int big_exact = 0;  // ZDL_BIG_EXACT=1: big traces skip big_simple (tests compare both paths)
+  int big_exact = 0;
+  bool wave_big = true;  // ZDL_WAVE_BIG=0: every big trace takes a workgroup (tests compare both)  // ZDL_BIG_EXACT=1: big traces skip big_simple (tests compare both paths)
   // host-API staging
   DevBuf<uint64_t> h_id, h_pid, h_off;
   DevBuf<int32_t> h_lsvc, h_rsvc, h_ip4, h_ip6;
@@ -1214,8 +1557,8 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
   if (e == hipSuccess) e = hipMemsetAsync(c->status.p, 0, 16, c->stream);
   if (e == hipSuccess && c->ord) e = c->first.ensure(SS);
   if (e == hipSuccess && c->ord) e = hipMemsetAsync(c->first.p, 0xff, SS * 8, c->stream);
-  if (e == hipSuccess) e = c->counters.ensure(5);  // + k_tail's finished-workgroup count
-  if (e == hipSuccess) e = hipMemsetAsync(c->counters.p, 0, 20, c->stream);
+  if (e == hipSuccess) e = c->counters.ensure(CTR_DONE + 1);  // + k_tail's finished-workgroup count
+  if (e == hipSuccess) e = hipMemsetAsync(c->counters.p, 0, (CTR_DONE + 1) * 4, c->stream);
   if (e == hipSuccess) e = hipHostMalloc((void**)&c->h_meta, 16, hipHostMallocDefault);
   // timing-only events: no system-scope fence (cache writeback) between the kernels they bracket
   for (int i = 0; i < 8 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->ev[i], hipEventDisableSystemFence);
@@ -1252,6 +1595,8 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
     c->skip = sk ? (uint32_t)strtoul(sk, nullptr, 0) : 0u;
     const char* be = getenv("ZDL_BIG_EXACT");
     c->big_exact = be && be[0] == '1';
+    const char* wb = getenv("ZDL_WAVE_BIG");
+    c->wave_big = !(wb && wb[0] == '0');
     const char* ft = getenv("ZDL_TM");
     if (ft) c->force_tm = !strcmp(ft, "hash") ? TM_HASH : (!strcmp(ft, "log") ? TM_LOG : -1);
   }
@@ -1284,7 +1629,7 @@ void zdl_destroy(zdl_ctx* c) {
   for (auto& r : c->rank) r.release();
   c->call.release(); c->errc.release(); c->status.release();
   c->first.release(); c->day_first.release(); c->o_key.release(); c->o_fa.release(); c->o_fb.release(); c->o_bfs.release();
-  c->big_list.release(); c->counters.release();
+  c->big_list.release(); c->counters.release(); c->retry.release();
   c->cx_win.release();
   if (c->prof_on && c->prof.p) {
     unsigned long long h[12] = {};
@@ -1423,19 +1768,21 @@ static bool plan_only_mode(const zdl_ctx* c) { return c->ord || c->days; }
 // listed with their start in lg and their link count.
 __global__ void k_seg_build(const uint64_t* __restrict__ lg_start, const uint32_t* __restrict__ lg_n, uint32_t W,
                             const uint32_t* __restrict__ big_list, const uint64_t* __restrict__ off,
-                            const uint32_t* __restrict__ tseg_big, uint32_t nb, const uint64_t* __restrict__ cx_win,
-                            const uint32_t* __restrict__ tseg_win, uint32_t nw, uint64_t tbase,
-                            uint64_t* __restrict__ src, uint32_t* __restrict__ cnt) {
+                            const uint32_t* __restrict__ tseg_big, uint32_t nb, uint32_t nl, uint32_t cap,
+                            const uint64_t* __restrict__ cx_win, const uint32_t* __restrict__ tseg_win, uint32_t nw,
+                            uint64_t tbase, uint64_t* __restrict__ src, uint32_t* __restrict__ cnt) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t nbl = (uint64_t)nb + nl;
   if (i < W) {
     src[i] = lg_start[i];
     cnt[i] = lg_n[i];
-  } else if (i < (uint64_t)W + nb) {
-    const uint32_t bi = (uint32_t)(i - W);
+  } else if (i < (uint64_t)W + nbl) {  // big_list's front (wave_big), then its back
+    const uint32_t j = (uint32_t)(i - W);
+    const uint32_t bi = j < nb ? j : cap - 1u - (j - nb);
     src[i] = tbase + 2 * off[big_list[bi]];
     cnt[i] = tseg_big[bi];
-  } else if (i < (uint64_t)W + nb + nw) {
-    const uint64_t k = i - W - nb;
+  } else if (i < (uint64_t)W + nbl + nw) {
+    const uint64_t k = i - W - nbl;
     src[i] = tbase + 2 * (cx_win[2 * k] & ((1ull << 48) - 1));
     cnt[i] = tseg_win[k];
   }
@@ -1456,17 +1803,18 @@ static int sparse_finish(zdl_ctx* c, uint32_t ep, uint32_t lW, uint64_t n_spans,
                          const uint64_t* off) {
   const hipStream_t s = c->stream;
   // how many big traces and queued windows k_tail logged (this put's counter slots)
-  HIP_TRY(c, hipMemcpyAsync(c->h_meta, c->counters.p + ep, 4, hipMemcpyDeviceToHost, s));
-  HIP_TRY(c, hipMemcpyAsync((uint32_t*)c->h_meta + 1, c->counters.p + 2 + ep, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipMemcpyAsync(c->h_meta, c->counters.p + ep * CTR_N, 4 * (CTR_LARGE + 1), hipMemcpyDeviceToHost, s));
   HIP_TRY(c, hipStreamSynchronize(s));
-  const uint32_t nb = ((uint32_t*)c->h_meta)[0], nw = ((uint32_t*)c->h_meta)[1];
-  if (nb > n_traces || nw > n_traces) return fail(c, ZDL_EDEVICE, "sparse: inconsistent tail counters");
-  const uint64_t nseg = (uint64_t)lW + nb + nw;
+  const uint32_t nb = ((uint32_t*)c->h_meta)[CTR_MID], nw = ((uint32_t*)c->h_meta)[CTR_CX],
+                 nl = ((uint32_t*)c->h_meta)[CTR_LARGE];
+  if ((uint64_t)nb + nl > n_traces || nw > n_traces) return fail(c, ZDL_EDEVICE, "sparse: inconsistent tail counters");
+  const uint64_t nseg = (uint64_t)lW + nb + nl + nw;
   HIP_TRY(c, c->seg_src.ensure(nseg));
   HIP_TRY(c, c->seg_n.ensure(nseg));
   HIP_TRY(c, c->seg_off.ensure(nseg));
   hipLaunchKernelGGL(k_seg_build, dim3((unsigned)((nseg + 255) / 256)), dim3(256), 0, s, c->lg_start.p, c->lg_n.p, lW,
-                     c->big_list.p, off, c->tseg_big.p, nb, c->cx_win.p, c->tseg_win.p, nw, (uint64_t)2 * n_spans,
+                     c->big_list.p, off, c->tseg_big.p, nb, nl, (uint32_t)n_traces, c->cx_win.p, c->tseg_win.p, nw,
+                     (uint64_t)2 * n_spans,
                      c->seg_src.p, c->seg_n.p);
   HIP_TRY(c, hipGetLastError());
   size_t need = 0;
@@ -1535,12 +1883,17 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   A.err = c->errc.p;
   A.big_list = c->big_list.p;
   const uint32_t ep = c->epoch & 1u;
-  A.big_count = c->counters.p + ep;
-  A.big_count_next = c->counters.p + (ep ^ 1u);
+  uint32_t* ctr = c->counters.p + ep * CTR_N;
+  A.big_count = ctr + CTR_MID;
+  A.large_count = ctr + CTR_LARGE;
+  A.tick_large = ctr + CTR_TICK_LARGE;
+  A.tick_mid = ctr + CTR_TICK_MID;
+  A.retry_count = ctr + CTR_RETRY;
+  A.ctr_next = c->counters.p + (ep ^ 1u) * CTR_N;
+  A.big_cap = (uint32_t)n_traces;
   A.status = c->status.p;
   A.small_max = WSMALL;
-  A.cx_count = c->counters.p + 2 + ep;
-  A.cx_count_next = c->counters.p + 2 + (ep ^ 1u);
+  A.cx_count = ctr + CTR_CX;
   A.cx_win = c->cx_win.p;
   A.skip = c->skip;
   A.prof = c->prof.p;
@@ -1605,6 +1958,12 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   A.b_hk = c->b_hk.p;
   A.b_hv = c->b_hv.p;
   A.skip_simple = c->big_exact;
+  // wave_big: not with insertion order / daily buckets (their big traces take the exact path)
+  A.wb_max = (c->wave_big && !c->big_exact && !c->ord && !c->days) ? (uint32_t)WB_MAX : 0u;
+  if (A.wb_max) {
+    HIP_TRY(c, c->retry.ensure(n_traces));
+    A.retry = c->retry.p;
+  }
   if (c->flags & ZDL_FLAG_TREE_EXPORT) {  // the last put's tree (insertion-order contexts only)
     HIP_TRY(c, c->tr_node.ensure(n_spans));
     HIP_TRY(c, c->tr_parent.ensure(n_spans));
@@ -1632,7 +1991,7 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   const bool ordered = SS <= (size_t)COMPACT_WG * 8 && !c->ord && !c->days && !c->sparse;
   if (ordered) HIP_TRY(c, ensure_map(c));
   A.map = ordered && !getenv("ZDL_NOTAILMAP") ? c->d_map : nullptr;
-  A.done = c->counters.p + 4;
+  A.done = c->counters.p + CTR_DONE;
   if (A.map) {
     A.flag = c->d_flag;
     A.seq = c->seq + 1;
@@ -1662,6 +2021,14 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   ev_record(c, 2);
   ev_record(c, 3);
   c->map_fresh = false;  // k_link has changed the table
+  if (A.wb_max) {  // big_list's front (WSMALL < n <= WB_MAX spans): one wave per trace
+    hipLaunchKernelGGL(k_mid, dim3((unsigned)c->cus * 4), dim3(MID_WG), 4 * WB_CARVE, c->stream, A);
+    const hipError_t me = hipGetLastError();
+    if (me != hipSuccess) {
+      c->poisoned = true;
+      return hip_fail(c, me, "k_mid launch");
+    }
+  }
   const hipError_t le = hipLaunchKernel(k_tail_fn(c->sparse ? 2 : dense, wmode, c->ord ? 1 : 0), dim3(grid),
                                         dim3(TAIL_WG), kargs, tail_block_bytes(wmode), c->stream);
   if (le != hipSuccess) {
@@ -2018,7 +2385,7 @@ int zdl_reset(zdl_ctx* c) {
   if (!c->sub.empty()) return group_each(c, [&](zdl_ctx* s) { return zdl_reset(s); });
   HIP_TRY(c, enter(c));
   if (c->poisoned) {  // the counter slots may hold a half-finished put's counts
-    HIP_TRY(c, hipMemsetAsync(c->counters.p, 0, 20, c->stream));
+    HIP_TRY(c, hipMemsetAsync(c->counters.p, 0, (CTR_DONE + 1) * 4, c->stream));
     c->poisoned = false;
   }
   const size_t SS = c->sparse ? 0 : (size_t)c->rows * c->S;  // sparse: only the status word
