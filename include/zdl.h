@@ -64,6 +64,13 @@ extern "C" {
 #define ZDL_DICT_SERVICE 0
 #define ZDL_DICT_IPV4    1
 #define ZDL_DICT_IPV6    2
+/* JSON v2 decoder keys (zdl_decode_json_v2): the raw JSON text of a service-name token (string
+ * content with its escapes, or a number's text: the binder unescapes and lower-cases it), an
+ * ipv4 address text as Endpoint keeps it (Endpoint.java:222-227), and - in the missing-key list
+ * only - an ipv6 address text, to be bound as its 16 bytes under ZDL_DICT_IPV6. */
+#define ZDL_DICT_JSON_SERVICE  3
+#define ZDL_DICT_JSON_IPV4     4
+#define ZDL_DICT_JSON_IPV6TEXT 5
 
 /* ---- output order for zdl_link ---- */
 #define ZDL_ORDER_SORTED      0  /* by (rank[parent], rank[child]) */
@@ -323,7 +330,20 @@ float        zdl_decoder_kernel_ms(const zdl_decoder* dec);  /* HIP-event time o
 int          zdl_decoder_missing(const zdl_decoder* dec, uint64_t i, int* dict, const uint8_t** key,
                                  uint32_t* len);
 int          zdl_decode_proto3(zdl_decoder* dec, const uint8_t* bytes, uint64_t len, zdl_decoded* out);
-int          zdl_decode_proto3_retry(zdl_decoder* dec, zdl_decoded* out);
+int          zdl_decode_proto3_retry(zdl_decoder* dec, zdl_decoded* out);  /* = zdl_decode_retry */
+/* Re-runs the last decode (proto3 or JSON v2) on the resident batch after binds. */
+int          zdl_decode_retry(zdl_decoder* dec, zdl_decoded* out);
+/* ---- JSON v2 ingest: SpanBytesDecoder.JSON_V2.decodeList(bytes)
+ * (codec/SpanBytesDecoder.java:94-120, internal/JsonCodec.java:142-155, internal/V2SpanReader.java
+ * over gson 2.8.5's strict JsonReader) decoded on the device to span columns. The same
+ * dictionary protocol as proto3 with the ZDL_DICT_JSON_* keys. Empty input or an empty array
+ * gives n_spans = 0 (the reference's empty list); ZDL_EREF_IAE where the reference throws
+ * IllegalArgumentException (the first failing span decides, as in the sequential read);
+ * ZDL_EINVAL for what the decoder does not restate: a timestamp / duration / port written as a
+ * fraction, exponent or out-of-range integer (the reference's Double.parseDouble fallback), an
+ * ip string with an escape, nesting deeper than 64 inside a span; batches up to 4 GiB. */
+int          zdl_decode_json_v2(zdl_decoder* dec, const uint8_t* bytes, uint64_t len, zdl_decoded* out);
+float        zdl_decoder_struct_ms(const zdl_decoder* dec);  /* HIP-event time of the last JSON structure passes */
 /* copies the last decode's device columns into the non-NULL host columns of dst */
 int          zdl_decoder_download(zdl_decoder* dec, const zdl_span_cols* dst);
 

@@ -1,0 +1,799 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY, NEVER A PRODUCT PATH.
+
+Literal CPU restatement of ``SpanBytesDecoder.JSON_V2.decodeList(bytes)`` and of the matching
+writer ``SpanBytesEncoder.JSON_V2``, used by ``tests/`` as the checker for the device decoder
+``zdl_decode_json_v2``. Nothing under ``zipkin_amd/`` imports it.
+
+Paths are relative to /root/reference/zipkin/src/main/java/zipkin2/:
+
+* ``read_list``      <- codec/SpanBytesDecoder.java:94-120 -> internal/JsonCodec.java:142-155
+                        (empty input -> false; beginArray; an empty array -> false; every element
+                        through the span reader; endArray; nothing after it is read)
+* ``_read_span``     <- internal/V2SpanReader.java:25-103 (+ Span.Builder, Span.java:402-619)
+* ``_read_endpoint`` <- internal/V2SpanReader.java:109-135 (+ Endpoint.Builder, Endpoint.java:132-260)
+* ``parse_ip``       <- Endpoint.Builder.parseIp(String) Endpoint.java:219-237, detectFamily
+                        :299-338, textToNumericFormatV6 :417-487, isValidIpV4Address :491-518,
+                        writeIpV6 :350-407
+* ``_Reader``        <- com.google.gson.stream.JsonReader 2.8.5 (zipkin/pom.xml:43-47; a
+                        third-party dependency absent from /root/reference), strict mode, as
+                        internal/JsonCodec.java:45-118 drives it: doPeek, nextNonWhitespace,
+                        peekKeyword (per-character case-insensitive true/false/null), peekNumber
+                        (no leading zeros; fitsInLong -> PEEKED_LONG, else PEEKED_NUMBER),
+                        nextQuotedValue / readEscapeCharacter, nextString (numbers as their text),
+                        nextLong / nextInt (quoted values through Long/Integer.parseInt), nextBoolean,
+                        skipValue — the published algorithm, restated
+* ``write_list``     <- internal/V2SpanWriter.java:88-160 + internal/JsonCodec.java:206-232,
+                        JsonEscaper.jsonEscape
+
+Errors: every exception the reference raises while reading becomes ``IllegalArgument`` (JsonCodec
+wraps them all, :152-153, :234-239). ``Unsupported`` marks the inputs the device decoder rejects
+with ZDL_EINVAL instead of restating them: a number the reference would have to pass through
+Double.parseDouble (a fraction or exponent, ``-0`` aside, or an integer outside long/int range,
+for ``timestamp``, ``duration``, annotation ``timestamp`` and ``port``), an ip string with a
+backslash escape, and objects/arrays nested deeper than 64 inside a span.
+
+Pinned by the reference's own vectors: SpanBytesDecoderTest JSON_V2 cases and V2SpanWriterTest
+(tests/test_json_v2.py transcribes them).
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Tuple
+
+from zipkin_amd.model import Endpoint, Kind, Span, format_ipv6, normalize_trace_id
+
+LONG_MIN, LONG_MAX = -(1 << 63), (1 << 63) - 1
+INT_MIN, INT_MAX = -(1 << 31), (1 << 31) - 1
+MAX_DEPTH = 64  # device decoder's nesting limit inside one span (Unsupported beyond)
+
+
+class IllegalArgument(Exception):
+    pass
+
+
+class Unsupported(Exception):
+    pass
+
+
+# gson JsonScope
+EMPTY_ARRAY, NONEMPTY_ARRAY, EMPTY_OBJECT, DANGLING_NAME, NONEMPTY_OBJECT, EMPTY_DOCUMENT, NONEMPTY_DOCUMENT = range(1, 8)
+# peeked tokens
+(P_NONE, P_BEGIN_OBJECT, P_END_OBJECT, P_BEGIN_ARRAY, P_END_ARRAY, P_TRUE, P_FALSE, P_NULL, P_DQ, P_LONG,
+ P_NUMBER, P_DQ_NAME, P_EOF) = range(13)
+
+
+def _wrap64(v: int) -> int:
+    v &= (1 << 64) - 1
+    return v - (1 << 64) if v >> 63 else v
+
+
+def _is_literal(c: str) -> bool:
+    """JsonReader.isLiteral; '/', '\\\\', ';', '#', '=' call checkLenient (strict: error)."""
+    if c in "/\\;#=":
+        raise IllegalArgument("Use JsonReader.setLenient(true) to accept malformed JSON")
+    return c not in "{}[]:, \t\f\r\n"
+
+
+class _Reader:
+    """com.google.gson.stream.JsonReader (strict) over the decoded characters."""
+
+    def __init__(self, text: str):
+        self.b = text
+        self.pos = 0
+        self.stack = [EMPTY_DOCUMENT]
+        self.peeked = P_NONE
+        self.peeked_long = 0
+        self.number_len = 0
+
+    # -- lexing
+    def _next_non_ws(self, throw_on_eof: bool):
+        b, p = self.b, self.pos
+        while p < len(b):
+            c = b[p]
+            p += 1
+            if c in " \n\t\r":
+                continue
+            self.pos = p
+            if c in "/#":  # comments: lenient only
+                raise IllegalArgument("Use JsonReader.setLenient(true) to accept malformed JSON")
+            return c
+        self.pos = p
+        if throw_on_eof:
+            raise IllegalArgument("End of input")
+        return None
+
+    def _do_peek(self) -> int:
+        top = self.stack[-1]
+        if top == EMPTY_ARRAY:
+            self.stack[-1] = NONEMPTY_ARRAY
+        elif top == NONEMPTY_ARRAY:
+            c = self._next_non_ws(True)
+            if c == "]":
+                self.peeked = P_END_ARRAY
+                return self.peeked
+            if c == ";":
+                raise IllegalArgument("lenient")
+            if c != ",":
+                raise IllegalArgument("Unterminated array")
+        elif top in (EMPTY_OBJECT, NONEMPTY_OBJECT):
+            self.stack[-1] = DANGLING_NAME
+            if top == NONEMPTY_OBJECT:
+                c = self._next_non_ws(True)
+                if c == "}":
+                    self.peeked = P_END_OBJECT
+                    return self.peeked
+                if c == ";":
+                    raise IllegalArgument("lenient")
+                if c != ",":
+                    raise IllegalArgument("Unterminated object")
+            c = self._next_non_ws(True)
+            if c == '"':
+                self.peeked = P_DQ_NAME
+                return self.peeked
+            if c == "}":
+                if top != NONEMPTY_OBJECT:
+                    self.peeked = P_END_OBJECT
+                    return self.peeked
+                raise IllegalArgument("Expected name")
+            raise IllegalArgument("lenient: unquoted or single-quoted name")
+        elif top == DANGLING_NAME:
+            self.stack[-1] = NONEMPTY_OBJECT
+            c = self._next_non_ws(True)
+            if c != ":":  # '=' / '=>' are lenient only
+                raise IllegalArgument("Expected ':'")
+        elif top == EMPTY_DOCUMENT:
+            self.stack[-1] = NONEMPTY_DOCUMENT
+        elif top == NONEMPTY_DOCUMENT:
+            c = self._next_non_ws(False)
+            if c is None:
+                self.peeked = P_EOF
+                return self.peeked
+            raise IllegalArgument("lenient: multiple top-level values")
+        c = self._next_non_ws(True)
+        if c == "]":
+            if top == EMPTY_ARRAY:
+                self.peeked = P_END_ARRAY
+                return self.peeked
+            raise IllegalArgument("lenient: ',]' or '[,'")  # falls into ',' / ';': checkLenient
+        if c in ";,":
+            if top in (EMPTY_ARRAY, NONEMPTY_ARRAY):
+                raise IllegalArgument("lenient: null from an empty array element")
+            raise IllegalArgument("Unexpected value")
+        if c == "'":
+            raise IllegalArgument("lenient: single-quoted string")
+        if c == '"':
+            self.peeked = P_DQ
+            return self.peeked
+        if c == "[":
+            self.peeked = P_BEGIN_ARRAY
+            return self.peeked
+        if c == "{":
+            self.peeked = P_BEGIN_OBJECT
+            return self.peeked
+        self.pos -= 1
+        r = self._peek_keyword()
+        if r != P_NONE:
+            return r
+        r = self._peek_number()
+        if r != P_NONE:
+            return r
+        if not _is_literal(self.b[self.pos]):
+            raise IllegalArgument("Expected value")
+        raise IllegalArgument("lenient: unquoted string")
+
+    def _peek_keyword(self) -> int:
+        b, p = self.b, self.pos
+        c = b[p]
+        if c in "tT":
+            kw, up, kind = "true", "TRUE", P_TRUE
+        elif c in "fF":
+            kw, up, kind = "false", "FALSE", P_FALSE
+        elif c in "nN":
+            kw, up, kind = "null", "NULL", P_NULL
+        else:
+            return P_NONE
+        for i in range(1, len(kw)):
+            if p + i >= len(b):
+                return P_NONE
+            if b[p + i] != kw[i] and b[p + i] != up[i]:
+                return P_NONE
+        if p + len(kw) < len(b) and _is_literal(b[p + len(kw)]):
+            return P_NONE  # "trues", "nullsoft"
+        self.pos = p + len(kw)
+        self.peeked = kind
+        return kind
+
+    def _peek_number(self) -> int:
+        """JsonReader.peekNumber (NUMBER_CHAR_* state machine)."""
+        b, p = self.b, self.pos
+        value, negative, fits, last, i = 0, False, True, 0, 0  # last: 0 none 1 sign 2 digit 3 decimal 4 fraction 5 exp-e 6 exp-sign 7 exp-digit
+        min_incomplete = -((1 << 63) // 10)  # Long.MIN_VALUE / 10, truncated toward zero
+        while True:
+            if p + i == len(b):
+                break
+            c = b[p + i]
+            if c == "-":
+                if last == 0:
+                    negative, last = True, 1
+                    i += 1
+                    continue
+                if last == 5:
+                    last = 6
+                    i += 1
+                    continue
+                return P_NONE
+            if c == "+":
+                if last == 5:
+                    last = 6
+                    i += 1
+                    continue
+                return P_NONE
+            if c in "eE":
+                if last in (2, 4):
+                    last = 5
+                    i += 1
+                    continue
+                return P_NONE
+            if c == ".":
+                if last == 2:
+                    last = 3
+                    i += 1
+                    continue
+                return P_NONE
+            if c < "0" or c > "9":
+                if not _is_literal(c):
+                    break
+                return P_NONE
+            if last in (0, 1):
+                value = -(ord(c) - 48)
+                last = 2
+            elif last == 2:
+                if value == 0:
+                    return P_NONE  # leading '0' prefix is not allowed
+                new = _wrap64(value * 10 - (ord(c) - 48))  # Java long arithmetic
+                fits = fits and (value > min_incomplete or (value == min_incomplete and new < value))
+                value = new
+            elif last == 3:
+                last = 4
+            elif last in (5, 6):
+                last = 7
+            i += 1
+        if last == 2 and fits and (value != LONG_MIN or negative) and (value != 0 or not negative):
+            self.peeked_long = value if negative else -value
+            self.pos = p + i
+            self.peeked = P_LONG
+            return P_LONG
+        if last in (2, 4, 7):
+            self.number_len = i
+            self.peeked = P_NUMBER
+            return P_NUMBER
+        return P_NONE
+
+    def _read_escape(self) -> str:
+        b = self.b
+        if self.pos == len(b):
+            raise IllegalArgument("Unterminated escape sequence")
+        e = b[self.pos]
+        self.pos += 1
+        if e == "u":
+            if self.pos + 4 > len(b):
+                raise IllegalArgument("Unterminated escape sequence")
+            r = 0
+            for c in b[self.pos:self.pos + 4]:
+                if not ("0" <= c <= "9" or "a" <= c <= "f" or "A" <= c <= "F"):
+                    raise IllegalArgument("\\u" + b[self.pos:self.pos + 4])  # NumberFormatException
+                r = r << 4 | int(c, 16)
+            self.pos += 4
+            return chr(r)
+        if e in "tbnrf":
+            return {"t": "\t", "b": "\b", "n": "\n", "r": "\r", "f": "\f"}[e]
+        if e in "\n'\"\\/":
+            return e
+        raise IllegalArgument("Invalid escape sequence")
+
+    def _quoted(self) -> Tuple[str, bool]:
+        """nextQuotedValue('"'); also says whether an escape was read."""
+        out, b, esc = [], self.b, False
+        while self.pos < len(b):
+            c = b[self.pos]
+            self.pos += 1
+            if c == '"':
+                return "".join(out), esc
+            if c == "\\":
+                esc = True
+                out.append(self._read_escape())
+            else:
+                out.append(c)
+        raise IllegalArgument("Unterminated string")
+
+    # -- the JsonReader API the codec uses
+    def peek(self) -> int:
+        return self.peeked if self.peeked != P_NONE else self._do_peek()
+
+    def begin_array(self):
+        if self.peek() != P_BEGIN_ARRAY:
+            raise IllegalArgument("Expected BEGIN_ARRAY")
+        self.stack.append(EMPTY_ARRAY)
+        self.peeked = P_NONE
+
+    def end_array(self):
+        if self.peek() != P_END_ARRAY:
+            raise IllegalArgument("Expected END_ARRAY")
+        self.stack.pop()
+        self.peeked = P_NONE
+
+    def begin_object(self):
+        if self.peek() != P_BEGIN_OBJECT:
+            raise IllegalArgument("Expected BEGIN_OBJECT")
+        self.stack.append(EMPTY_OBJECT)
+        self.peeked = P_NONE
+
+    def end_object(self):
+        if self.peek() != P_END_OBJECT:
+            raise IllegalArgument("Expected END_OBJECT")
+        self.stack.pop()
+        self.peeked = P_NONE
+
+    def has_next(self) -> bool:
+        p = self.peek()
+        return p not in (P_END_OBJECT, P_END_ARRAY, P_EOF)
+
+    def next_name(self) -> str:
+        if self.peek() != P_DQ_NAME:
+            raise IllegalArgument("Expected a name")
+        self.peeked = P_NONE
+        return self._quoted()[0]
+
+    def next_string_raw(self) -> Tuple[str, bool]:
+        p = self.peek()
+        if p == P_DQ:
+            self.peeked = P_NONE
+            return self._quoted()
+        if p == P_LONG:
+            self.peeked = P_NONE
+            return str(self.peeked_long), False
+        if p == P_NUMBER:
+            s = self.b[self.pos:self.pos + self.number_len]
+            self.pos += self.number_len
+            self.peeked = P_NONE
+            return s, False
+        raise IllegalArgument("Expected a string")
+
+    def next_string(self) -> str:
+        return self.next_string_raw()[0]
+
+    def peek_null(self) -> bool:
+        return self.peek() == P_NULL
+
+    def next_boolean(self) -> bool:
+        p = self.peek()
+        if p in (P_TRUE, P_FALSE):
+            self.peeked = P_NONE
+            return p == P_TRUE
+        raise IllegalArgument("Expected a boolean")
+
+    def _next_integral(self, lo: int, hi: int, parse) -> int:
+        p = self.peek()
+        if p == P_LONG:
+            self.peeked = P_NONE
+            v = self.peeked_long
+            if v < lo or v > hi:  # nextInt: (int) peekedLong != peekedLong
+                raise IllegalArgument("NumberFormatException")
+            return v
+        if p == P_NUMBER:
+            s = self.b[self.pos:self.pos + self.number_len]
+            self.pos += self.number_len
+            self.peeked = P_NONE
+            if s == "-0":  # Double.parseDouble("-0") == 0 exactly
+                return 0
+            raise Unsupported(f"number {s!r} goes through Double.parseDouble")
+        if p == P_DQ:
+            self.peeked = P_NONE
+            s, _ = self._quoted()
+            v = parse(s)
+            if v is None:
+                raise Unsupported(f"quoted number {s!r} goes through Double.parseDouble")
+            return v
+        raise IllegalArgument("Expected a long")
+
+    def next_long(self) -> int:
+        return self._next_integral(LONG_MIN, LONG_MAX, lambda s: _java_parse(s, LONG_MIN, LONG_MAX))
+
+    def next_int(self) -> int:
+        return self._next_integral(INT_MIN, INT_MAX, lambda s: _java_parse(s, INT_MIN, INT_MAX))
+
+    def skip_value(self):
+        count = 0
+        while True:
+            p = self.peek()
+            if p == P_BEGIN_ARRAY:
+                self.stack.append(EMPTY_ARRAY)
+                count += 1
+            elif p == P_BEGIN_OBJECT:
+                self.stack.append(EMPTY_OBJECT)
+                count += 1
+            elif p in (P_END_ARRAY, P_END_OBJECT):
+                self.stack.pop()
+                count -= 1
+            elif p in (P_DQ, P_DQ_NAME):
+                self._quoted()
+            elif p == P_NUMBER:
+                self.pos += self.number_len
+            if len(self.stack) - 2 > MAX_DEPTH:
+                raise Unsupported("nesting deeper than 64 inside a span")
+            self.peeked = P_NONE
+            if count == 0:
+                return
+
+
+def _java_parse(s: str, lo: int, hi: int) -> Optional[int]:
+    """Long.parseLong / Integer.parseInt (radix 10); None where they throw (the reference then
+    tries Double.parseDouble: Unsupported)."""
+    if not s:
+        return None
+    i = 1 if s[0] in "+-" else 0
+    if i == len(s) or not all("0" <= c <= "9" for c in s[i:]):
+        return None
+    v = int(s)
+    return v if lo <= v <= hi else None
+
+
+# ---- Endpoint.Builder.parseIp(String) ----
+
+def _not_hex(c: str) -> bool:
+    return not ("0" <= c <= "9" or "a" <= c <= "f" or "A" <= c <= "F")
+
+
+def _ipv4_word(s: str, a: int, b: int) -> bool:
+    n = b - a
+    if n < 1 or n > 3 or s[a] < "0":
+        return False
+    if n == 3:
+        c0, c1, c2 = s[a], s[a + 1], s[a + 2]
+        return c1 >= "0" and c2 >= "0" and ((c0 <= "1" and c1 <= "9" and c2 <= "9") or
+                                            (c0 == "2" and c1 <= "5" and (c2 <= "5" or (c1 < "5" and c2 <= "9"))))
+    return s[a] <= "9" and (n == 1 or "0" <= s[a + 1] <= "9")
+
+
+def _valid_ipv4(s: str, a: int, b: int) -> bool:
+    """isValidIpV4Address(ip, from, toExcluded) (netty NetUtil, Endpoint.java:491-499)."""
+    if not (7 <= b - a <= 15):
+        return False
+    i = s.find(".", a + 1)
+    if i <= 0 or not _ipv4_word(s, a, i):
+        return False
+    f = i + 2
+    i = s.find(".", f)
+    if i <= 0 or not _ipv4_word(s, f - 1, i):
+        return False
+    f = i + 2
+    i = s.find(".", f)
+    if i <= 0 or not _ipv4_word(s, f - 1, i):
+        return False
+    return _ipv4_word(s, i + 1, b)
+
+
+def detect_family(s: str) -> str:
+    has_colon = has_dot = False
+    for c in s:
+        if c == ".":
+            has_dot = True
+        elif c == ":":
+            if has_dot:
+                return "unknown"
+            has_colon = True
+        elif _not_hex(c):
+            return "unknown"
+    if has_colon:
+        if has_dot:
+            last = s.rfind(":")
+            if not _valid_ipv4(s, last + 1, len(s)):
+                return "unknown"
+            if last == 1 and s[0] == ":":
+                return "v4embedded"
+            if last != 6 or s[0] != ":" or s[1] != ":":
+                return "unknown"
+            if any(c not in "fF0" for c in s[2:6]):
+                return "unknown"
+            return "v4embedded"
+        return "v6"
+    if has_dot and _valid_ipv4(s, 0, len(s)):
+        return "v4"
+    return "unknown"
+
+
+def text_to_v6(s: str) -> Optional[bytes]:
+    """textToNumericFormatV6 (Guava InetAddresses 23, Endpoint.java:417-487)."""
+    parts = s.split(":")
+    if len(parts) > 10:  # String.split(":", 10): the tenth part keeps the rest
+        parts = parts[:9] + [":".join(parts[9:])]
+    if len(parts) < 3 or len(parts) > 9:
+        return None
+    skip = -1
+    for i in range(1, len(parts) - 1):
+        if parts[i] == "":
+            if skip >= 0:
+                return None
+            skip = i
+    if skip >= 0:
+        hi, lo = skip, len(parts) - skip - 1
+        if parts[0] == "":
+            hi -= 1
+            if hi != 0:
+                return None
+        if parts[-1] == "":
+            lo -= 1
+            if lo != 0:
+                return None
+    else:
+        hi, lo = len(parts), 0
+    skipped = 8 - (hi + lo)
+    if not (skipped >= 1 if skip >= 0 else skipped == 0):
+        return None
+    out = bytearray()
+
+    def hextet(p):
+        if p == "" or any(_not_hex(c) for c in p):
+            return None
+        v = int(p, 16)
+        return v if v <= 0xFFFF else None  # Integer.parseInt overflow also throws
+
+    for i in range(hi):
+        v = hextet(parts[i])
+        if v is None:
+            return None
+        out += v.to_bytes(2, "big")
+    out += bytes(2 * skipped)
+    for i in range(lo, 0, -1):
+        v = hextet(parts[len(parts) - i])
+        if v is None:
+            return None
+        out += v.to_bytes(2, "big")
+    return bytes(out)
+
+
+def parse_ip(s: str, ipv4: Optional[str], ipv6: Optional[str]) -> Tuple[Optional[str], Optional[str]]:
+    """Endpoint.Builder.parseIp(String): the builder's (ipv4, ipv6) after the call."""
+    if not s:
+        return ipv4, ipv6
+    fam = detect_family(s)
+    if fam == "v4":
+        return s, ipv6
+    if fam == "v4embedded":
+        return s[s.rfind(":") + 1:], ipv6
+    if fam == "v6":
+        b = text_to_v6(s)
+        if b is None:
+            return ipv4, ipv6
+        return ipv4, format_ipv6(b)
+    return ipv4, ipv6
+
+
+# ---- V2SpanReader ----
+
+def _read_endpoint(r: _Reader) -> Optional[Endpoint]:
+    r.begin_object()
+    svc, ipv4, ipv6, port = None, None, None, 0
+    while r.has_next():
+        name = r.next_name()
+        if r.peek_null():
+            r.skip_value()
+            continue
+        if name == "serviceName":
+            s = r.next_string()
+            svc = None if not s else s.lower()  # toLowerCase(Locale.ROOT); non-ASCII unpinned
+        elif name in ("ipv4", "ipv6"):
+            s, esc = r.next_string_raw()
+            if esc:
+                raise Unsupported("ip string with an escape")
+            ipv4, ipv6 = parse_ip(s, ipv4, ipv6)
+        elif name == "port":
+            p = r.next_int()
+            if p > 0xFFFF:
+                raise IllegalArgument(f"invalid port {p}")
+            port = max(p, 0)
+        else:
+            r.skip_value()
+    r.end_object()
+    e = Endpoint(svc, ipv4, ipv6, port)
+    return None if e.is_empty() else e  # Span.Builder.localEndpoint: EMPTY_ENDPOINT -> null
+
+
+_KINDS = {"CLIENT": Kind.CLIENT, "SERVER": Kind.SERVER, "PRODUCER": Kind.PRODUCER, "CONSUMER": Kind.CONSUMER}
+
+
+def _check_hex(s: str):
+    if any(not ("0" <= c <= "9" or "a" <= c <= "f") for c in s):
+        raise IllegalArgument(f"{s} should be lower-hex encoded with no prefix")
+    return None
+
+
+def _read_span(r: _Reader) -> Span:
+    r.begin_object()
+    trace_id = sid = None
+    pid = None
+    kind = None
+    name = None
+    ts = dur = 0
+    local = remote = None
+    ann = []
+    tags = {}
+    shared = debug = None
+    while r.has_next():
+        key = r.next_name()
+        if key == "traceId":  # Span.Builder.traceId -> normalizeTraceId (Span.java:402-405, 634-649)
+            try:
+                trace_id = normalize_trace_id(r.next_string())
+            except ValueError as ex:
+                raise IllegalArgument(str(ex))
+            continue
+        if key == "id":
+            sid = _id_norm(r.next_string())
+            continue
+        if r.peek_null():
+            r.skip_value()
+            continue
+        if key == "parentId":
+            pid = _parent_id_norm(r.next_string())
+        elif key == "kind":
+            k = r.next_string()
+            if k not in _KINDS:  # Span.Kind.valueOf
+                raise IllegalArgument(f"No enum constant zipkin2.Span.Kind.{k}")
+            kind = _KINDS[k]
+        elif key == "name":
+            name = r.next_string()
+        elif key == "timestamp":
+            ts = r.next_long()
+        elif key == "duration":
+            dur = r.next_long()
+        elif key == "localEndpoint":
+            local = _read_endpoint(r)
+        elif key == "remoteEndpoint":
+            remote = _read_endpoint(r)
+        elif key == "annotations":
+            r.begin_array()
+            while r.has_next():
+                r.begin_object()
+                at = av = None
+                while r.has_next():
+                    n = r.next_name()
+                    if n == "timestamp":
+                        at = r.next_long()
+                    elif n == "value":
+                        av = r.next_string()
+                    else:
+                        r.skip_value()
+                if at is None or av is None:
+                    raise IllegalArgument("Incomplete annotation")
+                r.end_object()
+                ann.append((at, av))
+            r.end_array()
+        elif key == "tags":
+            r.begin_object()
+            while r.has_next():
+                k = r.next_name()
+                if r.peek_null():
+                    raise IllegalArgument("No value at $.tags." + k)
+                tags[k] = r.next_string()
+            r.end_object()
+        elif key == "debug":
+            if r.next_boolean():
+                debug = True
+        elif key == "shared":
+            if r.next_boolean():
+                shared = True
+        else:
+            r.skip_value()
+    r.end_object()
+    if trace_id is None or sid is None:  # Span.Builder.build: IllegalStateException
+        raise IllegalArgument("Missing :" + (" traceId" if trace_id is None else "") + (" id" if sid is None else ""))
+    return Span.create(trace_id, sid, pid, kind, name=name, timestamp=max(ts, 0), duration=max(dur, 0),
+                       local_endpoint=local, remote_endpoint=remote, annotations=tuple(ann),
+                       tags=tags, shared=shared, debug=debug)
+
+
+def _id_norm(s: str) -> str:
+    if len(s) == 0:
+        raise IllegalArgument("id is empty")
+    if len(s) > 16:
+        raise IllegalArgument("id.length > 16")
+    _check_hex(s)
+    if s == "0" * 16:
+        raise IllegalArgument("id is all zeros")
+    return s.rjust(16, "0")
+
+
+def _parent_id_norm(s: str) -> Optional[str]:
+    if len(s) == 0:
+        raise IllegalArgument("parentId is empty")
+    if len(s) > 16:
+        raise IllegalArgument("parentId.length > 16")
+    _check_hex(s)
+    return None if s.strip("0") == "" else s.rjust(16, "0")
+
+
+def read_list(data: bytes) -> List[Span]:
+    """SpanBytesDecoder.JSON_V2.decodeList(bytes): [] for empty input or an empty array; raises
+    IllegalArgument / Unsupported."""
+    if len(data) == 0:
+        return []
+    r = _Reader(data.decode("utf-8", "replace"))  # InputStreamReader(UTF_8); malformed -> U+FFFD
+    try:
+        r.begin_array()
+        if not r.has_next():
+            return []
+        out = []
+        while r.has_next():
+            out.append(_read_span(r))
+        r.end_array()
+        return out
+    except IndexError:  # reading past the end of the characters
+        raise IllegalArgument("End of input")
+
+
+# ---- V2SpanWriter (SpanBytesEncoder.JSON_V2) ----
+
+def json_escape(v: str) -> str:
+    """JsonEscaper.jsonEscape: '"', '\\\\', control characters below 0x20 (\\b \\f \\n \\r \\t as
+    themselves, others \\u00XX), U+2028 and U+2029."""
+    out = []
+    for c in v:
+        o = ord(c)
+        if c == '"':
+            out.append('\\"')
+        elif c == "\\":
+            out.append("\\\\")
+        elif o < 0x20:
+            out.append({8: "\\b", 9: "\\t", 10: "\\n", 12: "\\f", 13: "\\r"}.get(o, "\\u%04x" % o))
+        elif o in (0x2028, 0x2029):
+            out.append("\\u%04x" % o)
+        else:
+            out.append(c)
+    return "".join(out)
+
+
+def write_endpoint(e: Endpoint) -> str:
+    parts = []
+    if e.service_name is not None:
+        parts.append('"serviceName":"%s"' % json_escape(e.service_name))
+    if e.ipv4 is not None:
+        parts.append('"ipv4":"%s"' % e.ipv4)
+    if e.ipv6 is not None:
+        parts.append('"ipv6":"%s"' % e.ipv6)
+    if e.port:
+        parts.append('"port":%d' % e.port)
+    return "{" + ",".join(parts) + "}"
+
+
+def write_span(s: Span) -> str:
+    o = ['{"traceId":"%s"' % s.trace_id]
+    if s.parent_id is not None:
+        o.append(',"parentId":"%s"' % s.parent_id)
+    o.append(',"id":"%s"' % s.id)
+    if s.kind is not None:
+        o.append(',"kind":"%s"' % Kind(s.kind).name)
+    if s.name is not None:
+        o.append(',"name":"%s"' % json_escape(s.name))
+    if s.timestamp:
+        o.append(',"timestamp":%d' % s.timestamp)
+    if s.duration:
+        o.append(',"duration":%d' % s.duration)
+    if s.local_endpoint is not None:
+        o.append(',"localEndpoint":' + write_endpoint(s.local_endpoint))
+    if s.remote_endpoint is not None:
+        o.append(',"remoteEndpoint":' + write_endpoint(s.remote_endpoint))
+    if s.annotations:
+        o.append(',"annotations":[' + ",".join('{"timestamp":%d,"value":"%s"}' % (t, json_escape(v))
+                                               for t, v in s.annotations) + "]")
+    if s.tags:
+        o.append(',"tags":{' + ",".join('"%s":"%s"' % (json_escape(k), json_escape(v)) for k, v in s.tags) + "}")
+    if s.debug:
+        o.append(',"debug":true')
+    if s.shared:
+        o.append(',"shared":true')
+    o.append("}")
+    return "".join(o)
+
+
+def write_list(spans) -> bytes:
+    """SpanBytesEncoder.JSON_V2.encodeList: "[]" when empty, else the spans joined by ','."""
+    return ("[" + ",".join(write_span(s) for s in spans) + "]").encode("utf-8")

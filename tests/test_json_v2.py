@@ -1,0 +1,461 @@
+"""JSON v2 ingest: the oracle restatement (gson 2.8.5 strict JsonReader +
+V2SpanReader + V2SpanWriter) pinned by the reference's own vectors (CPU), and the device decoder
+zdl_decode_json_v2 checked exactly against it (GPU): same columns, same dictionary ids, same
+errors, and storage queries fed by accept_json_v2 answering like accept(decodeList(bytes)).
+
+Reference vectors transcribed (zipkin/src/test/java/zipkin2/codec/): SpanBytesEncoderTest
+span_JSON_V2 / localSpan_JSON_V2 / span_64bitTraceId_JSON_V2 / span_shared_JSON_V2 /
+specialCharsInJson_JSON_V2 / span_minimum_JSON_V2 / span_noLocalServiceName_JSON_V2 /
+span_noRemoteServiceName_JSON_V2 (exact bytes, decoded back to the same span), and every
+SpanBytesDecoderTest JSON_V2 case (niceErrorOnUppercase_traceId, readsTraceIdHighFromTraceIdField,
+ignoresNull_topLevelFields, ignoresNull_endpoint_topLevelFields, skipsIncompleteEndpoint,
+niceErrorOnIncomplete_annotation, niceErrorOnNull_traceId / _id / _tagValue / _annotationValue /
+_annotationTimestamp, readSpan_local/remoteEndpoint_noServiceName, falseOnEmpty_inputSpans,
+niceErrorOnMalformed_inputSpans, traceRoundTrip / spansRoundTrip over the golden traces).
+Parity unpinned (no reference-executed result): non-ASCII case mapping of service names, malformed
+UTF-8 replacement counts, surrogate escapes in names; the gson restatement itself beyond those
+vectors (gson is a dependency absent from the reference tree).
+"""
+import random
+
+import numpy as np
+import pytest
+
+from golden_io import load, spans
+from oracle import json_oracle as J
+from test_proto3 import COLS, SVC, assert_same, fresh, rand_batch
+from zipkin_amd.columnar import pack_traces
+from zipkin_amd.model import Endpoint, Kind, Span
+
+DL = load("dependency_linker.json")
+ST = load("storage_dependencies.json")
+GOLDEN_SPANS = [s for c in DL["cases"] for t in c["traces"] for s in spans(t)]
+
+TODAY = 1472470996199  # TestObjects.TODAY as the encoder tests print it (ms)
+CLIENT_SPAN = Span.create(
+    "7180c278b62e8f6a216a2aea45d08fc9", "5b4185666d50f68b", "6b221d5bc9e6496c", Kind.CLIENT, name="get",
+    timestamp=1472470996199000, duration=207000,
+    local_endpoint=Endpoint.create("frontend", "127.0.0.1"),
+    remote_endpoint=Endpoint.create("backend", "192.168.99.101", 9000),
+    annotations=((1472470996238000, "foo"), (1472470996403000, "bar")),
+    tags={"clnt/finagle.version": "6.45.0", "http.path": "/api"})
+LOCAL_SPAN = Span.create("dc955a1d4768875d", "dc955a1d4768875d", None, None, name="encode",
+                         timestamp=1510256710021866, duration=1117,
+                         local_endpoint=Endpoint.create("isao01", "10.23.14.72"))
+UTF8_SPAN = Span.create("1", "1", None, None, name="\"\\\t\b\n\r\f",
+                        annotations=((1, "\u2028 and \u2029"),),
+                        tags={"\"foo": "Database error: ORA-00942:\u2028 and \u2029 table or view does not exist\n"})
+_BODY = (',"kind":"CLIENT","name":"get","timestamp":1472470996199000,"duration":207000,'
+         '"localEndpoint":{"serviceName":"frontend","ipv4":"127.0.0.1"},'
+         '"remoteEndpoint":{"serviceName":"backend","ipv4":"192.168.99.101","port":9000},'
+         '"annotations":[{"timestamp":1472470996238000,"value":"foo"},{"timestamp":1472470996403000,"value":"bar"}],'
+         '"tags":{"clnt/finagle.version":"6.45.0","http.path":"/api"}')
+ENCODER_VECTORS = [  # SpanBytesEncoderTest: (span, exact JSON_V2 bytes)
+    (CLIENT_SPAN, '{"traceId":"7180c278b62e8f6a216a2aea45d08fc9","parentId":"6b221d5bc9e6496c","id":"5b4185666d50f68b"'
+     + _BODY + "}"),
+    (LOCAL_SPAN, '{"traceId":"dc955a1d4768875d","id":"dc955a1d4768875d","name":"encode","timestamp":1510256710021866,'
+     '"duration":1117,"localEndpoint":{"serviceName":"isao01","ipv4":"10.23.14.72"}}'),
+    (CLIENT_SPAN.to_builder(trace_id="216a2aea45d08fc9"),
+     '{"traceId":"216a2aea45d08fc9","parentId":"6b221d5bc9e6496c","id":"5b4185666d50f68b"' + _BODY + "}"),
+    (CLIENT_SPAN.to_builder(kind=Kind.SERVER, shared=True),
+     '{"traceId":"7180c278b62e8f6a216a2aea45d08fc9","parentId":"6b221d5bc9e6496c","id":"5b4185666d50f68b"'
+     + _BODY.replace('"CLIENT"', '"SERVER"') + ',"shared":true}'),
+    (UTF8_SPAN, '{"traceId":"0000000000000001","id":"0000000000000001","name":"\\"\\\\\\t\\b\\n\\r\\f",'
+     '"annotations":[{"timestamp":1,"value":"\\u2028 and \\u2029"}],"tags":{"\\"foo":"Database error: '
+     'ORA-00942:\\u2028 and \\u2029 table or view does not exist\\n"}}'),
+    (Span.create("7180c278b62e8f6a216a2aea45d08fc9", "5b4185666d50f68b"),
+     '{"traceId":"7180c278b62e8f6a216a2aea45d08fc9","id":"5b4185666d50f68b"}'),
+    (CLIENT_SPAN.to_builder(local_endpoint=Endpoint.create(None, "127.0.0.1")),
+     '{"traceId":"7180c278b62e8f6a216a2aea45d08fc9","parentId":"6b221d5bc9e6496c","id":"5b4185666d50f68b"'
+     + _BODY.replace('{"serviceName":"frontend","ipv4":"127.0.0.1"}', '{"ipv4":"127.0.0.1"}') + "}"),
+    (CLIENT_SPAN.to_builder(remote_endpoint=Endpoint.create(None, "192.168.99.101", 9000)),
+     '{"traceId":"7180c278b62e8f6a216a2aea45d08fc9","parentId":"6b221d5bc9e6496c","id":"5b4185666d50f68b"'
+     + _BODY.replace('{"serviceName":"backend","ipv4":"192.168.99.101","port":9000}',
+                     '{"ipv4":"192.168.99.101","port":9000}') + "}"),
+]
+
+_ID = '  "traceId": "6b221d5bc9e6496c",\n'
+DECODER_VECTORS = [  # SpanBytesDecoderTest JSON_V2: (span object, None = IllegalArgumentException, else check)
+    ('{\n  "traceId": "48485A3953BB6124",\n  "name": "get-traces",\n  "id": "6b221d5bc9e6496c"\n}', None),
+    ('{\n' + _ID + '  "parentId": null,\n  "id": "6b221d5bc9e6496c",\n  "name": null,\n  "timestamp": null,\n'
+     '  "duration": null,\n  "localEndpoint": null,\n  "remoteEndpoint": null,\n  "annotations": null,\n'
+     '  "tags": null,\n  "debug": null,\n  "shared": null\n}', lambda s: s.id == "6b221d5bc9e6496c"),
+    ('{\n' + _ID + '  "name": "get-traces",\n  "id": "6b221d5bc9e6496c",\n  "localEndpoint": {\n'
+     '    "serviceName": null,\n    "ipv4": "127.0.0.1",\n    "ipv6": null,\n    "port": null\n  }\n}',
+     lambda s: s.local_endpoint == Endpoint.create(None, "127.0.0.1")),
+    ('{\n' + _ID + '  "id": "6b221d5bc9e6496c",\n  "localEndpoint": {\n    "serviceName": null,\n'
+     '    "ipv4": null,\n    "ipv6": null,\n    "port": null\n  }\n}', lambda s: s.local_endpoint is None),
+    ('{\n' + _ID + '  "id": "6b221d5bc9e6496c",\n  "localEndpoint": {\n  }\n}', lambda s: s.local_endpoint is None),
+    ('{\n' + _ID + '  "id": "6b221d5bc9e6496c",\n  "remoteEndpoint": {\n    "serviceName": null,\n'
+     '    "ipv4": null,\n    "ipv6": null,\n    "port": null\n  }\n}', lambda s: s.remote_endpoint is None),
+    ('{\n' + _ID + '  "id": "6b221d5bc9e6496c",\n  "remoteEndpoint": {\n  }\n}', lambda s: s.remote_endpoint is None),
+    ('{\n' + _ID + '  "name": "get-traces",\n  "id": "6b221d5bc9e6496c",\n  "annotations": [\n'
+     '    { "timestamp": 1472470996199000}\n  ]\n}', None),
+    ('{\n  "traceId": null,\n  "name": "get-traces",\n  "id": "6b221d5bc9e6496c"\n}', None),
+    ('{\n' + _ID + '  "name": "get-traces",\n  "id": null\n}', None),
+    ('{\n' + _ID + '  "name": "get-traces",\n  "id": "6b221d5bc9e6496c",\n  "tags": {\n    "foo": NULL\n  }\n}', None),
+    ('{\n' + _ID + '  "name": "get-traces",\n  "id": "6b221d5bc9e6496c",\n  "annotations": [\n'
+     '    { "timestamp": 1472470996199000, "value": NULL}\n  ]\n}', None),
+    ('{\n' + _ID + '  "name": "get-traces",\n  "id": "6b221d5bc9e6496c",\n  "annotations": [\n'
+     '    { "timestamp": NULL, "value": "foo"}\n  ]\n}', None),
+    ('{\n' + _ID + '  "name": "get-traces",\n  "id": "6b221d5bc9e6496c",\n  "localEndpoint": {\n'
+     '    "ipv4": "127.0.0.1"\n  }\n}', lambda s: s.local_service_name is None),
+    ('{\n' + _ID + '  "name": "get-traces",\n  "id": "6b221d5bc9e6496c",\n  "remoteEndpoint": {\n'
+     '    "ipv4": "127.0.0.1"\n  }\n}', lambda s: s.remote_service_name is None),
+]
+
+
+# ---------------- oracle vs the reference's vectors (CPU) ----------------
+
+@pytest.mark.parametrize("k", range(len(ENCODER_VECTORS)))
+def test_writer_and_reader_vectors(k):  # SpanBytesEncoderTest *_JSON_V2 + the decoder round trips
+    span, text = ENCODER_VECTORS[k]
+    assert J.write_span(span) == text
+    assert J.read_list(("[" + text + "]").encode()) == [span]
+
+
+@pytest.mark.parametrize("k", range(len(DECODER_VECTORS)))
+def test_decoder_vectors(k):  # SpanBytesDecoderTest *_JSON_V2 (decodeOne of the object, as a list)
+    obj, check = DECODER_VECTORS[k]
+    data = ("[" + obj + "]").encode()
+    if check is None:
+        with pytest.raises(J.IllegalArgument):
+            J.read_list(data)
+    else:
+        (s,) = J.read_list(data)
+        assert check(s)
+
+
+def test_trace_id_high_read_from_trace_id_field():  # readsTraceIdHighFromTraceIdField
+    a = J.read_list(b'[{"traceId": "48485a3953bb61246b221d5bc9e6496c", "name": "get-traces", "id": "6b221d5bc9e6496c"}]')
+    b = J.read_list(b'[{"traceId": "6b221d5bc9e6496c", "name": "get-traces", "id": "6b221d5bc9e6496c"}]')
+    assert a == [b[0].to_builder(trace_id="48485a3953bb61246b221d5bc9e6496c")]
+
+
+def test_empty_and_malformed():  # falseOnEmpty_inputSpans / niceErrorOnMalformed_inputSpans
+    assert J.read_list(b"") == []
+    assert J.read_list(b"[]") == []
+    with pytest.raises(J.IllegalArgument):
+        J.read_list(b"hello")
+
+
+def test_golden_traces_round_trip():  # traceRoundTrip_JSON_V2 / spansRoundTrip_JSON_V2
+    assert J.read_list(J.write_list(GOLDEN_SPANS)) == GOLDEN_SPANS
+
+
+@pytest.mark.parametrize("text,v4,v6", [
+    ("127.0.0.1", "127.0.0.1", None), ("01.2.3.4", "01.2.3.4", None), ("1.2.3", None, None),
+    ("::1", None, "::1"), ("::1.2.3.4", "1.2.3.4", None), ("::ffff:1.2.3.4", "1.2.3.4", None),
+    ("::fFfF:1.2.3.4", "1.2.3.4", None), ("::ffff:102:304", None, "::ffff:102:304"),
+    ("2001:db8::c001", None, "2001:db8::c001"), ("2001:DB8:0:0:0:0:0:C001", None, "2001:db8::c001"),
+    ("1::2::3", None, None), ("1:2:3:4:5:6:7:8", None, "1:2:3:4:5:6:7:8"), ("1:2:3:4:5:6:7:8:9", None, None),
+    ("::", None, "::"), (":1::", None, None), ("00000001::", None, "1::"), ("10000::", None, None),
+    ("1.2.3.256", None, None), ("abc", None, None), ("::1.2.3.4:5", None, None),
+])
+def test_parse_ip(text, v4, v6):  # Endpoint.Builder.parseIp(String) restated (Endpoint.java:219-518)
+    assert J.parse_ip(text, None, None) == (v4, v6)
+
+
+def test_gson_strictness():
+    ok = b'[{"traceId":"1","id":"2"}]'
+    assert len(J.read_list(ok)) == 1
+    for bad in [b'[{"traceId":"1","id":"2"},]', b'[{"traceId":"1","id":"2",}]', b"[{'traceId':'1','id':'2'}]",
+                b'[{traceId:"1","id":"2"}]', b'[{"traceId":"1";"id":"2"}]', b'[{"traceId"="1","id":"2"}]',
+                b'[{"traceId":"1","id":"2"} {"traceId":"1","id":"2"}]', b'[/*c*/{"traceId":"1","id":"2"}]',
+                b'[{"traceId":"1","id":"2","x":01}]', b'[{"traceId":"1","id":"2","x":tru}]',
+                b'[{"traceId":"1","id":"2","x":"\\x"}]', b'[{"traceId":"1","id":"2","x":"\\u12g4"}]',
+                b'[{"traceId":"1","id":"2"}', b'[{"traceId":"1","id":"2","x":[1,]}]']:
+        with pytest.raises(J.IllegalArgument):
+            J.read_list(bad)
+    # accepted by the strict reader: keywords in either case per character, trailing input
+    # after the array, escapes in names, numbers as strings, quoted longs
+    assert J.read_list(b'[{"traceId":"1","id":"2","shared":tRuE}] trailing') == \
+        [Span.create("1", "2", shared=True)]
+    assert J.read_list(b'[{"trace\\u0049d":123,"id":"2","timestamp":"77"}]') == [Span.create("123", "2", timestamp=77)]
+    with pytest.raises(J.Unsupported):
+        J.read_list(b'[{"traceId":"1","id":"2","timestamp":1.5}]')
+
+
+# ---------------- generators: gson-legal formatting variety ----------------
+
+WS = [" ", "\n", "\t", "\r", "  "]
+
+
+def _ws(r):
+    return "".join(r.choice(WS) for _ in range(r.randrange(3))) if r.random() < 0.3 else ""
+
+
+def _esc_some(r, s: str) -> str:
+    """A JSON string literal for s, with some characters written as \\u escapes."""
+    out = []
+    for c in J.json_escape(s):
+        out.append("\\u%04x" % ord(c) if c.isalnum() and r.random() < 0.1 else c)
+    return '"' + "".join(out) + '"'
+
+
+def _kw(r, v: str) -> str:
+    return "".join(c.upper() if r.random() < 0.3 else c for c in v)
+
+
+def _junk_value(r, depth=0):
+    k = r.randrange(7)
+    if k == 0 and depth < 3:
+        return "[" + ",".join(_junk_value(r, depth + 1) for _ in range(r.randrange(3))) + "]"
+    if k == 1 and depth < 3:
+        return "{" + ",".join(_esc_some(r, "k%d" % i) + ":" + _junk_value(r, depth + 1) for i in range(r.randrange(3))) + "}"
+    return r.choice(['"x\\"y"', "12", "-3.5e2", _kw(r, "true"), _kw(r, "null"), "0", '"\\u00e9"', "-0"])
+
+
+def _endpoint(r, e: Endpoint) -> str:
+    m = []
+    if e.service_name is not None:
+        svc = "".join(c.upper() if r.random() < 0.3 else c for c in e.service_name)
+        m.append(('"serviceName"', _esc_some(r, svc)))
+    if e.ipv4 is not None:
+        m.append(('"ipv4"' if r.random() < 0.8 else '"ipv6"', '"%s"' % e.ipv4))
+    if e.ipv6 is not None:
+        m.append(('"ipv6"', '"%s"' % (e.ipv6.upper() if r.random() < 0.3 else e.ipv6)))
+    if e.port:
+        m.append(('"port"', str(e.port) if r.random() < 0.8 else '"%d"' % e.port))
+    if r.random() < 0.2:
+        m.append(('"serviceName"' if not e.service_name else '"extra"', _kw(r, "null")))
+    if r.random() < 0.2:
+        m.append(('"whatever"', _junk_value(r)))
+    r.shuffle(m)
+    return "{" + ",".join(_ws(r) + k + _ws(r) + ":" + _ws(r) + v + _ws(r) for k, v in m) + "}"
+
+
+def noisy_span(r, s: Span) -> str:
+    m = [('"traceId"', '"%s"' % (s.trace_id if r.random() < 0.8 else s.trace_id.lstrip("0") or "0")),
+         ('"id"', '"%s"' % s.id)]
+    if s.parent_id:
+        m.append(('"parentId"', '"%s"' % s.parent_id))
+    elif r.random() < 0.2:
+        m.append(('"parentId"', _kw(r, "null")))
+    if s.kind is not None:
+        m.append(('"kind"', _esc_some(r, Kind(s.kind).name)))
+    if s.name:
+        m.append(('"name"', _esc_some(r, s.name)))
+    if s.timestamp:
+        m.append(('"timestamp"', str(s.timestamp) if r.random() < 0.8 else '"%d"' % s.timestamp))
+    if s.duration:
+        m.append(('"duration"', str(s.duration)))
+    if s.local_endpoint:
+        m.append(('"localEndpoint"', _endpoint(r, s.local_endpoint)))
+    if s.remote_endpoint:
+        m.append(('"remoteEndpoint"', _endpoint(r, s.remote_endpoint)))
+    if s.annotations:
+        m.append(('"annotations"', "[" + ",".join('{"value":%s,"timestamp":%d}' % (_esc_some(r, v), t)
+                                                  for t, v in s.annotations) + "]"))
+    if s.tags:
+        m.append(('"tags"', "{" + ",".join(_esc_some(r, k) + ":" + _esc_some(r, v) for k, v in s.tags) + "}"))
+    if s.shared:
+        m.append(('"shared"', _kw(r, "true")))
+    elif r.random() < 0.1:
+        m.append(('"shared"', _kw(r, "false")))
+    if s.debug:
+        m.append(('"debug"', _kw(r, "true")))
+    if r.random() < 0.3:
+        m.append(('"unknown%d"' % r.randrange(9), _junk_value(r)))
+    if r.random() < 0.2:
+        m.append(('"tr\\u0061ceId"', '"%s"' % s.trace_id))  # an escaped name, the same value again
+    r.shuffle(m)
+    return "{" + ",".join(_ws(r) + k + _ws(r) + ":" + _ws(r) + v + _ws(r) for k, v in m) + "}"
+
+
+def noisy_list(r, sp) -> bytes:
+    return (_ws(r) + "[" + ",".join(_ws(r) + noisy_span(r, s) + _ws(r) for s in sp) + "]" + _ws(r)).encode()
+
+
+def oracle_columns(data, svc, ip4, ip6):
+    return pack_traces([[s] for s in J.read_list(data)], svc, ip4, ip6)
+
+
+def mutate(r, data: bytes) -> bytes:
+    b = bytearray(data)
+    for _ in range(r.randrange(1, 3)):
+        k = r.randrange(5)
+        i = r.randrange(len(b)) if b else 0
+        if k == 0 and b:
+            b[i] = ord(r.choice('{}[]:,"\\ 0a-.eE'))
+        elif k == 1 and b:
+            del b[i:]
+        elif k == 2:
+            b.insert(i, ord(r.choice('{}[]:,"\\ ')))
+        elif k == 3 and b:
+            del b[i]
+        elif b:
+            b[i] = r.randrange(256)
+    return bytes(b)
+
+
+def test_noisy_lists_decode_like_the_spans():
+    r = random.Random(11)
+    for _ in range(30):
+        sp = rand_batch(r, r.randrange(1, 20))
+        # (against the plain encoding: Endpoint.create's ipv6 text is Python's, writeIpV6 differs
+        # for a zero run after an earlier one, e.g. 2001:db8::1:0:0:0)
+        assert J.read_list(noisy_list(r, sp)) == J.read_list(J.write_list(sp))
+
+
+def test_oracle_fuzz_never_crashes():
+    r = random.Random(7)
+    for _ in range(300):
+        d = mutate(r, noisy_list(r, rand_batch(r, 3)))
+        try:
+            J.read_list(d)
+        except (J.IllegalArgument, J.Unsupported):
+            pass
+
+
+# ---------------- device decoder vs oracle (GPU) ----------------
+
+def _dec(d):
+    from zipkin_amd.jsonv2 import JsonV2Decoder
+    return JsonV2Decoder(*d)
+
+
+@pytest.mark.gpu
+def test_gpu_decode_reference_vectors():
+    from zipkin_amd import _native as N
+    d, o = fresh(), fresh()
+    dec = _dec(d)
+    for span, text in ENCODER_VECTORS:
+        data = ("[" + text + "]").encode()
+        assert_same(dec.decode_columns(data), oracle_columns(data, *o))
+    for obj, check in DECODER_VECTORS:
+        data = ("[" + obj + "]").encode()
+        if check is None:
+            with pytest.raises(N.ReferenceIllegalArgumentException):
+                dec.decode(data)
+        else:
+            assert_same(dec.decode_columns(data), oracle_columns(data, *o))
+    assert [x.strings for x in d] == [x.strings for x in o]
+    dec.close()
+
+
+@pytest.mark.gpu
+def test_gpu_decode_golden_spans():
+    d, o = fresh(), fresh()
+    dec = _dec(d)
+    data = J.write_list(GOLDEN_SPANS)
+    assert_same(dec.decode_columns(data), oracle_columns(data, *o))
+    assert [x.strings for x in d] == [x.strings for x in o]
+    dec.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(12))
+def test_gpu_decode_random_batches(seed):
+    """Several noisy batches through one decoder: ids stay first-seen across batches."""
+    r = random.Random(seed)
+    d, o = fresh(), fresh()
+    dec = _dec(d)
+    for _ in range(3):
+        sp = rand_batch(r, r.randrange(1, 400))
+        data = noisy_list(r, sp) if seed % 2 else J.write_list(sp)
+        assert_same(dec.decode_columns(data), oracle_columns(data, *o))
+        assert [x.strings for x in d] == [x.strings for x in o]
+    dec.close()
+
+
+@pytest.mark.gpu
+def test_gpu_decode_errors_match_oracle():
+    """Mutated batches: the device raises where the reference throws, rejects what it does not
+    restate (ZDL_EINVAL), and otherwise decodes identically."""
+    from zipkin_amd import _native as N
+    r = random.Random(99)
+    seen = {"ok": 0, "iae": 0, "unsupported": 0}
+    for _ in range(500):
+        d, o = fresh(), fresh()
+        dec = _dec(d)
+        data = mutate(r, noisy_list(r, rand_batch(r, r.randrange(1, 6))))
+        try:
+            exp = oracle_columns(data, *o)
+            kind = "ok"
+        except J.IllegalArgument:
+            kind = "iae"
+        except J.Unsupported:
+            kind = "unsupported"
+        seen[kind] += 1
+        if kind == "iae":
+            with pytest.raises(N.ReferenceIllegalArgumentException):
+                dec.decode_columns(data)
+        elif kind == "unsupported":
+            with pytest.raises(N.ZdlError) as ei:
+                dec.decode_columns(data)
+            assert ei.value.code == N.ZDL_EINVAL
+        else:
+            assert_same(dec.decode_columns(data), exp)
+            assert [x.strings for x in d] == [x.strings for x in o]
+        dec.close()
+    assert min(seen.values()) > 0, seen
+
+
+@pytest.mark.gpu
+def test_gpu_decode_edge_inputs():
+    from zipkin_amd import _native as N
+    dec = _dec(fresh())
+    one = b'{"traceId":"1","id":"2"}'
+    for data in (b"", b"[]", b" \n[ \t]", b"[]junk", b"  [  ]  ]"):
+        assert dec.decode(data).n_spans == 0, data
+    for data in (b"hello", b"[", b"[ ", b"{}", b"[1]", b"[[]]", b"[" + one, b"[" + one + b",]", b"[" + one + one + b"]",
+                 b"[" + one + b"," + one, b"[null]", b"[" + one + b"}", b"[" + one + b", 1]", b"[1, " + one + b"]",
+                 b"/*x*/[" + one + b"]", b"[" + one.replace(b"}", b',"a":{"b":[}]}') + b"]"):
+        with pytest.raises(N.ReferenceIllegalArgumentException):
+            dec.decode(data)
+    assert dec.decode(b"[" + b",".join([one] * 3) + b"] trailing {[").n_spans == 3
+    deep = b"[" + one[:-1] + b',"x":' + b"[" * 70 + b"]" * 70 + b"}]"
+    with pytest.raises(N.ZdlError) as ei:
+        dec.decode(deep)
+    assert ei.value.code == N.ZDL_EINVAL
+    ok = b"[" + one[:-1] + b',"x":' + b"[" * 60 + b"]" * 60 + b"}]"
+    assert dec.decode(ok).n_spans == 1
+    dec.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ST["cases"], ids=lambda c: c["name"])
+def test_gpu_storage_accept_json_v2(case):
+    """ITDependencies through accept_json_v2(encode(batch)) == the transcribed expectations."""
+    from golden_io import check_links
+    from zipkin_amd.storage import InMemoryStorage
+    store = InMemoryStorage(strict_trace_id=True)
+    for b in case["batches"]:
+        store.accept_json_v2(J.write_list(spans(b))).execute()
+    for q in case["queries"]:
+        check_links(store.get_dependencies(q["endTs"], q["lookback"]).execute(), q["expect"], "only")
+    store.close()
+
+
+@pytest.mark.gpu
+def test_gpu_decode_then_link_large():
+    """20k traces of noisy JSON: decode on the device, link the device columns (grouped on the
+    device), same links as packing the oracle-decoded spans; objects beyond the LDS window too."""
+    from zipkin_amd import _native as N
+    r = random.Random(5)
+    sp = []
+    for t in range(20000):
+        tid = "%016x" % r.randrange(1, 1 << 64)
+        root = r.randrange(1, 1 << 64)
+        sp.append(Span.create(tid, root, None, Kind.SERVER, local_endpoint=Endpoint.create(r.choice(SVC))))
+        for _ in range(4):
+            sp.append(Span.create(tid, r.randrange(1, 1 << 64), root, r.choice([Kind.CLIENT, None]),
+                                  local_endpoint=Endpoint.create(r.choice(SVC) + ("x" * 3000 if r.random() < 0.01 else "")),
+                                  remote_endpoint=Endpoint.create(r.choice(SVC)),
+                                  tags={"error": ""} if r.random() < 0.05 else None))
+    r.shuffle(sp)
+    data = noisy_list(r, sp)
+    d, o = fresh(), fresh()
+    dec = _dec(d)
+    b = dec.decode(data)
+    ctx = N.Context(len(d[0]))
+    ctx.put_spans_device({k: getattr(b.dev, k) for k in COLS}, b.n_spans, None, 0)
+    got = sorted(zip(*(a.tolist() for a in ctx.link())))
+    exp_cols = oracle_columns(data, *o)
+    ctx2 = N.Context(len(o[0]))
+    ctx2.put_spans_ungrouped(exp_cols)
+    exp = sorted(zip(*(a.tolist() for a in ctx2.link())))
+    assert got == exp and len(got) > 0
+    assert dec.kernel_ms() > 0 and dec.struct_ms() > 0
+    dec.close()

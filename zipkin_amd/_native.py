@@ -13,6 +13,8 @@ LIB_PATH = os.environ.get("ZDL_LIB_PATH") or os.path.join(HERE, "libzdl.so")  # 
 
 ZDL_OK, ZDL_EINVAL, ZDL_ENOMEM, ZDL_EDEVICE, ZDL_EREF_NPE, ZDL_EREF_IAE = 0, -1, -2, -3, -4, -5
 ZDL_DICT_SERVICE, ZDL_DICT_IPV4, ZDL_DICT_IPV6 = 0, 1, 2
+# JSON v2 keys (include/zdl.h): raw service token text, ipv4 text, ipv6 text (missing list only)
+ZDL_DICT_JSON_SERVICE, ZDL_DICT_JSON_IPV4, ZDL_DICT_JSON_IPV6TEXT = 3, 4, 5
 ZDL_ORDER_SORTED, ZDL_ORDER_FIRST_SEEN, ZDL_ORDER_INSERTION = 0, 1, 2
 ZDL_FLAG_TIMING = 1
 ZDL_FLAG_TIMING_ALL = 2
@@ -40,7 +42,7 @@ EXPORTS = (
     "zdl_decoder_dict_size", "zdl_decoder_missing", "zdl_decode_proto3", "zdl_decode_proto3_retry",
     "zdl_decoder_download", "zdl_decoder_kernel_ms", "zdl_put_mysql_rows", "zdl_rows_last_error",
     "zdl_comm_unique_id", "zdl_comm_init", "zdl_put_spans_device_multi", "zdl_device_count", "zdl_shard_of",
-    "zdl_tree_export",
+    "zdl_tree_export", "zdl_decode_json_v2", "zdl_decode_retry", "zdl_decoder_struct_ms",
 )
 ZDL_ABI_VERSION = 2
 ZDL_COMM_ID_BYTES = 128
@@ -166,6 +168,10 @@ def lib() -> C.CDLL:
                                       C.POINTER(u32)]
     L.zdl_decode_proto3.argtypes = [vp, C.c_char_p, u64, C.POINTER(Decoded)]
     L.zdl_decode_proto3_retry.argtypes = [vp, C.POINTER(Decoded)]
+    L.zdl_decode_json_v2.argtypes = [vp, C.c_char_p, u64, C.POINTER(Decoded)]
+    L.zdl_decode_retry.argtypes = [vp, C.POINTER(Decoded)]
+    L.zdl_decoder_struct_ms.restype = C.c_float
+    L.zdl_decoder_struct_ms.argtypes = [vp]
     L.zdl_decoder_download.argtypes = [vp, C.POINTER(SpanCols)]
     L.zdl_put_mysql_rows.argtypes = [vp, C.POINTER(MysqlRows), u64, vp, u32]
     L.zdl_put_mysql_rows.restype = C.c_int
@@ -187,7 +193,7 @@ def lib() -> C.CDLL:
     L.zdl_decoder_kernel_ms.restype = C.c_float
     L.zdl_decoder_kernel_ms.argtypes = [vp]
     for name in ("zdl_decoder_bind", "zdl_decoder_missing", "zdl_decode_proto3", "zdl_decode_proto3_retry",
-                 "zdl_decoder_download"):
+                 "zdl_decoder_download", "zdl_decode_json_v2", "zdl_decode_retry"):
         getattr(L, name).restype = C.c_int
     for name in ("zdl_set_ranks", "zdl_set_window", "zdl_put_spans", "zdl_put_spans_device", "zdl_sync",
                  "zdl_link", "zdl_merge_links", "zdl_add_links", "zdl_reset", "zdl_table_export",
@@ -440,7 +446,8 @@ class Store:
 
 
 class Decoder:
-    """zdl_decoder: proto3 ListOfSpans -> device span columns (zdl_decode_proto3)."""
+    """zdl_decoder: proto3 ListOfSpans / JSON v2 span lists -> device span columns
+    (zdl_decode_proto3, zdl_decode_json_v2)."""
 
     def __init__(self, device: int = 0):
         L = lib()
@@ -463,9 +470,14 @@ class Decoder:
         self.check(self._L.zdl_decode_proto3(self.h, bytes(data), len(data), C.byref(out)))
         return out
 
+    def decode_json(self, data: bytes) -> Decoded:
+        out = Decoded()
+        self.check(self._L.zdl_decode_json_v2(self.h, bytes(data), len(data), C.byref(out)))
+        return out
+
     def retry(self) -> Decoded:
         out = Decoded()
-        self.check(self._L.zdl_decode_proto3_retry(self.h, C.byref(out)))
+        self.check(self._L.zdl_decode_retry(self.h, C.byref(out)))
         return out
 
     def missing(self, n: int):
@@ -493,6 +505,9 @@ class Decoder:
 
     def kernel_ms(self) -> float:
         return float(self._L.zdl_decoder_kernel_ms(self.h))
+
+    def struct_ms(self) -> float:
+        return float(self._L.zdl_decoder_struct_ms(self.h))
 
     def close(self):
         if getattr(self, "h", None):

@@ -26,6 +26,7 @@
 // misaligned position; not supported here).
 
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cstring>
@@ -463,6 +464,8 @@ __global__ void __launch_bounds__(kBlock) k_proto3_spans(const uint8_t* __restri
   o.ts[i] = ts;
 }
 
+#include "zdl_json.inc"
+
 template <class T>
 struct DBuf {
   T* p = nullptr;
@@ -552,8 +555,19 @@ struct zdl_decoder {
   HBuf<uint64_t> lo_h;
   HBuf<int64_t> ts_h;
   std::vector<std::string> missing;  // kind byte + key bytes, first-seen order
-  hipEvent_t ev[2] = {nullptr, nullptr};  // around the last k_proto3_spans
+  hipEvent_t ev[2] = {nullptr, nullptr};  // around the last k_proto3_spans / k_js_spans
   float kernel_ms = 0.f;
+  int fmt = 0;  // the resident batch: 0 proto3, 1 JSON v2
+  // JSON v2 structure (zdl_json.inc)
+  DBuf<int4> js_fn, js_gfn;
+  DBuf<unsigned long long> js_gst, js_misc;  // misc: [0] E (the array's closing bracket), [1] spans before E
+  DBuf<uint32_t> js_cnt;
+  DBuf<uint64_t> js_off, js_starts;
+  DBuf<uint8_t> js_tmp;  // hipCUB scan scratch
+  HBuf<unsigned long long> js_h;
+  uint64_t js_open = 0;  // the opening '['
+  float struct_ms = 0.f;  // HIP-event time of the structural passes of the last JSON decode
+  hipEvent_t ev_s[2] = {nullptr, nullptr};
 };
 
 namespace {
@@ -613,14 +627,24 @@ int run_kernel(zdl_decoder* d, zdl_decoded* out) {
     Out o{d->lo.p,   d->id.p, d->pid.p, d->lsvc.p,     d->rsvc.p,     d->ip4.p,    d->ip6.p,
           d->pf.p,   d->ts.p, d->miss.p, d->miss_off.p, d->miss_len.p, d->status.p, (uint32_t*)(d->status.p + 1)};
     DEC_TRY(d, hipEventRecord(d->ev[0], s));
-    k_proto3_spans<<<(unsigned)((n + kBlock - 1) / kBlock), kBlock, 0, s>>>(d->buf.p, d->len, d->start.p, d->slen.p, (uint32_t)n,
-                                                                dict, o);
+    if (d->fmt == 1)
+      zjs::k_js_spans<<<(unsigned)((n + zjs::kSpanWG - 1) / zjs::kSpanWG), zjs::kSpanWG, 0, s>>>(
+          d->buf.p, d->len, d->js_starts.p, (uint32_t)n, d->js_open, d->js_misc.p, dict, o);
+    else
+      k_proto3_spans<<<(unsigned)((n + kBlock - 1) / kBlock), kBlock, 0, s>>>(d->buf.p, d->len, d->start.p, d->slen.p,
+                                                                              (uint32_t)n, dict, o);
     DEC_TRY(d, hipGetLastError());
     DEC_TRY(d, hipEventRecord(d->ev[1], s));
     DEC_TRY(d, hipMemcpyAsync(d->status_h.p, d->status.p, 16, hipMemcpyDeviceToHost, s));
     DEC_TRY(d, hipStreamSynchronize(s));
     DEC_TRY(d, hipEventElapsedTime(&d->kernel_ms, d->ev[0], d->ev[1]));
     const unsigned long long fe = d->status_h.p[0];
+    if (fe != kNoErr && d->fmt == 1)  // (span << 2 | after-the-span << 1 | iae): the lowest decides
+      return (fe & 1) ? dfail(d, ZDL_EREF_IAE, "reference throws IllegalArgumentException reading List<Span> from json (span " +
+                                                   std::to_string(fe >> 2) + ((fe & 2) ? ", after it)" : ")"))
+                      : dfail(d, ZDL_EINVAL, "json v2: span " + std::to_string(fe >> 2) +
+                                                 " holds a number the reference parses through Double.parseDouble, an ip "
+                                                 "with an escape or nesting deeper than 64 (not supported)");
     if (fe != kNoErr)  // the first failing span decides, before the scan's own verdict
       return (fe & 1) ? dfail(d, ZDL_EREF_IAE, "reference throws IllegalArgumentException reading List<Span> from proto3 (span " +
                                                    std::to_string(fe >> 1) + ")")
@@ -643,13 +667,15 @@ int run_kernel(zdl_decoder* d, zdl_decoded* out) {
     DEC_TRY(d, hipStreamSynchronize(s));
     d->missing.clear();
     std::unordered_map<std::string, bool> seen;
-    static const int kind_of[4] = {ZDL_DICT_SERVICE, ZDL_DICT_IPV4, ZDL_DICT_IPV6, ZDL_DICT_SERVICE};
+    static const int kind_of[2][4] = {{ZDL_DICT_SERVICE, ZDL_DICT_IPV4, ZDL_DICT_IPV6, ZDL_DICT_SERVICE},
+                                      {ZDL_DICT_JSON_SERVICE, ZDL_DICT_JSON_IPV4, ZDL_DICT_JSON_IPV6TEXT,
+                                       ZDL_DICT_JSON_SERVICE}};
     for (uint64_t i = 0; i < n; ++i) {
       for (int sl = 0; m[i] && sl < 4; ++sl) {
         if (!(m[i] >> sl & 1)) continue;
-        std::string k(1, (char)kind_of[sl]);
+        std::string k(1, (char)kind_of[d->fmt][sl]);
         const uint64_t off = mo[4 * i + sl];
-        if (sl == SLOT_LIP4) {
+        if (sl == SLOT_LIP4 && d->fmt == 0) {
           for (int b = 3; b >= 0; --b) k.push_back((char)(uint8_t)(off >> (8 * b)));
         } else {
           k.append((const char*)raw.data() + off, ml[4 * i + sl]);
@@ -684,7 +710,8 @@ zdl_decoder* zdl_decoder_create(int device) {
   d->device = device;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess ||
       d->status.ensure(2) != hipSuccess || d->status_h.ensure(2) != hipSuccess ||
-      hipEventCreate(&d->ev[0]) != hipSuccess || hipEventCreate(&d->ev[1]) != hipSuccess) {
+      hipEventCreate(&d->ev[0]) != hipSuccess || hipEventCreate(&d->ev[1]) != hipSuccess ||
+      hipEventCreate(&d->ev_s[0]) != hipSuccess || hipEventCreate(&d->ev_s[1]) != hipSuccess) {
     if (d->stream) (void)hipStreamDestroy(d->stream);
     delete d;
     return nullptr;
@@ -699,6 +726,8 @@ void zdl_decoder_destroy(zdl_decoder* d) {
   hipStream_t s = d->stream;
   for (hipEvent_t e : d->ev)
     if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : d->ev_s)
+    if (e) (void)hipEventDestroy(e);
   delete d;  // buffers free themselves
   if (s) (void)hipStreamDestroy(s);
 }
@@ -706,7 +735,7 @@ void zdl_decoder_destroy(zdl_decoder* d) {
 const char* zdl_decoder_last_error(const zdl_decoder* d) { return d ? d->err.c_str() : "null decoder"; }
 
 int zdl_decoder_bind(zdl_decoder* d, int kind, const uint8_t* key, uint32_t len, int32_t id) {
-  if (!d || (len && !key) || id < 0 || kind < ZDL_DICT_SERVICE || kind > ZDL_DICT_IPV6)
+  if (!d || (len && !key) || id < 0 || kind < ZDL_DICT_SERVICE || kind > ZDL_DICT_JSON_IPV4)
     return dfail(d, ZDL_EINVAL, "zdl_decoder_bind: bad argument");
   if ((kind == ZDL_DICT_IPV4 && len != 4) || (kind == ZDL_DICT_IPV6 && len != 16) || len == 0)
     return dfail(d, ZDL_EINVAL, "zdl_decoder_bind: key length");
@@ -720,6 +749,8 @@ int zdl_decoder_bind(zdl_decoder* d, int kind, const uint8_t* key, uint32_t len,
 uint64_t zdl_decoder_dict_size(const zdl_decoder* d) { return d ? d->keys.size() : 0; }
 
 float zdl_decoder_kernel_ms(const zdl_decoder* d) { return d ? d->kernel_ms : 0.f; }
+
+float zdl_decoder_struct_ms(const zdl_decoder* d) { return d ? d->struct_ms : 0.f; }
 
 int zdl_decoder_missing(const zdl_decoder* d, uint64_t i, int* kind, const uint8_t** key, uint32_t* len) {
   if (!d || i >= d->missing.size() || !kind || !key || !len) return ZDL_EINVAL;
@@ -736,6 +767,7 @@ int zdl_decode_proto3(zdl_decoder* d, const uint8_t* data, uint64_t len, zdl_dec
   (void)hipGetLastError();
   DEC_TRY(d, hipSetDevice(d->device));
   d->missing.clear();
+  d->fmt = 0;
   const hipStream_t s = d->stream;
   // the batch goes up straight from the caller's bytes while a host thread runs the top-level
   // scan (Proto3Codec.readList / SpanField.read: key tossed / readLengthPrefix) over them
@@ -791,6 +823,103 @@ int zdl_decode_proto3(zdl_decoder* d, const uint8_t* data, uint64_t len, zdl_dec
     DEC_TRY(d, d->miss_off.ensure(4 * n));
     DEC_TRY(d, d->miss_len.ensure(4 * n));
   }
+  return run_kernel(d, out);
+}
+
+int zdl_decode_retry(zdl_decoder* d, zdl_decoded* out) {
+  if (!d || !out) return dfail(d, ZDL_EINVAL, "zdl_decode_retry: null argument");
+  (void)hipGetLastError();
+  DEC_TRY(d, hipSetDevice(d->device));
+  d->missing.clear();
+  return run_kernel(d, out);
+}
+
+int zdl_decode_json_v2(zdl_decoder* d, const uint8_t* data, uint64_t len, zdl_decoded* out) {
+  using namespace zjs;
+  if (!d || !out || (len && !data)) return dfail(d, ZDL_EINVAL, "zdl_decode_json_v2: null argument");
+  if (len > (uint64_t)kBlk * kGroup * 1024) return dfail(d, ZDL_EINVAL, "zdl_decode_json_v2: batch limited to 4 GiB");
+  (void)hipGetLastError();
+  DEC_TRY(d, hipSetDevice(d->device));
+  std::memset(out, 0, sizeof(*out));
+  d->missing.clear();
+  d->fmt = 1;
+  d->n = 0;
+  d->len = len;
+  d->scan_rc = ZDL_OK;
+  d->struct_ms = 0.f;
+  if (len == 0) return ZDL_OK;  // JsonCodec.readList: empty input -> false -> emptyList
+  // beginArray: the first token must be '[' (whitespace before it; comments are lenient-only)
+  uint64_t p0 = 0;
+  while (p0 < len && (data[p0] == ' ' || data[p0] == '\n' || data[p0] == '\t' || data[p0] == '\r')) ++p0;
+  if (p0 == len || data[p0] != '[')
+    return dfail(d, ZDL_EREF_IAE, "reference throws IllegalArgumentException reading List<Span> from json (no array)");
+  d->js_open = p0;
+  const hipStream_t s = d->stream;
+  const uint32_t nblk = (uint32_t)((len + kBlk - 1) / kBlk);
+  const uint32_t ngroup = (nblk + kGroup - 1) / kGroup;
+  DEC_TRY(d, d->buf.ensure(len));
+  DEC_TRY(d, hipMemcpyAsync(d->buf.p, data, len, hipMemcpyHostToDevice, s));
+  DEC_TRY(d, d->js_fn.ensure(nblk));
+  DEC_TRY(d, d->js_gfn.ensure(ngroup));
+  DEC_TRY(d, d->js_gst.ensure(ngroup));
+  DEC_TRY(d, d->js_cnt.ensure(nblk));
+  DEC_TRY(d, d->js_off.ensure(nblk));
+  DEC_TRY(d, d->js_misc.ensure(2));
+  DEC_TRY(d, d->js_h.ensure(2));
+  size_t tmp = 0;
+  DEC_TRY(d, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, d->js_cnt.p, d->js_off.p, (int)nblk, s));
+  DEC_TRY(d, d->js_tmp.ensure(tmp));
+  DEC_TRY(d, hipEventRecord(d->ev_s[0], s));
+  DEC_TRY(d, hipMemsetAsync(d->js_misc.p, 0xFF, 8, s));
+  DEC_TRY(d, hipMemsetAsync(d->js_misc.p + 1, 0, 8, s));
+  const unsigned g4 = (unsigned)((nblk + 3) / 4);
+  k_js_fn<<<g4, 256, 0, s>>>(d->buf.p, len, nblk, d->js_fn.p);
+  k_js_group<<<ngroup, 1024, 0, s>>>(d->js_fn.p, nblk, d->js_gfn.p);
+  k_js_top<<<1, 1024, 0, s>>>(d->js_gfn.p, ngroup, d->js_gst.p);
+  k_js_starts<0><<<g4, 256, 0, s>>>(d->buf.p, len, nblk, d->js_fn.p, d->js_gst.p, d->js_cnt.p, nullptr, nullptr,
+                                     d->js_misc.p);
+  DEC_TRY(d, hipGetLastError());
+  DEC_TRY(d, hipcub::DeviceScan::ExclusiveSum(d->js_tmp.p, tmp, d->js_cnt.p, d->js_off.p, (int)nblk, s));
+  uint64_t last_off = 0;
+  uint32_t last_cnt = 0;
+  DEC_TRY(d, hipMemcpyAsync(&last_off, d->js_off.p + nblk - 1, 8, hipMemcpyDeviceToHost, s));
+  DEC_TRY(d, hipMemcpyAsync(&last_cnt, d->js_cnt.p + nblk - 1, 4, hipMemcpyDeviceToHost, s));
+  DEC_TRY(d, hipStreamSynchronize(s));
+  const uint64_t total = last_off + last_cnt;
+  if (total) {
+    DEC_TRY(d, d->js_starts.ensure(total));
+    k_js_starts<1><<<g4, 256, 0, s>>>(d->buf.p, len, nblk, d->js_fn.p, d->js_gst.p, nullptr, d->js_off.p,
+                                       d->js_starts.p, d->js_misc.p);
+    k_js_before<<<(unsigned)((total + 255) / 256), 256, 0, s>>>(d->js_starts.p, total, d->js_misc.p, d->js_misc.p + 1);
+    DEC_TRY(d, hipGetLastError());
+  }
+  DEC_TRY(d, hipEventRecord(d->ev_s[1], s));
+  DEC_TRY(d, hipMemcpyAsync(d->js_h.p, d->js_misc.p, 16, hipMemcpyDeviceToHost, s));
+  DEC_TRY(d, hipStreamSynchronize(s));
+  DEC_TRY(d, hipEventElapsedTime(&d->struct_ms, d->ev_s[0], d->ev_s[1]));
+  const uint64_t E = d->js_h.p[0], n = d->js_h.p[1];
+  if (n == 0) {  // "[ ]" (hasNext false) is the empty list; anything else in it is not a span object
+    if (E == ~0ull)
+      return dfail(d, ZDL_EREF_IAE, "reference throws IllegalArgumentException reading List<Span> from json (End of input)");
+    for (uint64_t p = p0 + 1; p < E; ++p)
+      if (!(data[p] == ' ' || data[p] == '\n' || data[p] == '\t' || data[p] == '\r'))
+        return dfail(d, ZDL_EREF_IAE, "reference throws IllegalArgumentException reading List<Span> from json (element 0)");
+    return ZDL_OK;
+  }
+  if (n >= (1ull << 31)) return dfail(d, ZDL_EINVAL, "zdl_decode_json_v2: at most 2^31 spans per batch");
+  d->n = n;
+  DEC_TRY(d, d->lo.ensure(n));
+  DEC_TRY(d, d->id.ensure(n));
+  DEC_TRY(d, d->pid.ensure(n));
+  DEC_TRY(d, d->lsvc.ensure(n));
+  DEC_TRY(d, d->rsvc.ensure(n));
+  DEC_TRY(d, d->ip4.ensure(n));
+  DEC_TRY(d, d->ip6.ensure(n));
+  DEC_TRY(d, d->pf.ensure(n));
+  DEC_TRY(d, d->ts.ensure(n));
+  DEC_TRY(d, d->miss.ensure(n));
+  DEC_TRY(d, d->miss_off.ensure(4 * n));
+  DEC_TRY(d, d->miss_len.ensure(4 * n));
   return run_kernel(d, out);
 }
 

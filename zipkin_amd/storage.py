@@ -84,6 +84,7 @@ class InMemoryStorage:
         self._ts = np.zeros(0, np.int64)
         self._alive = np.zeros(0, bool)
         self._decoder = None  # proto3.Proto3Decoder, created on the first accept_proto3
+        self._json_decoder = None  # jsonv2.JsonV2Decoder, created on the first accept_json_v2
 
     @staticmethod
     def new_builder():
@@ -179,6 +180,25 @@ class InMemoryStorage:
         return Call(lambda: None)
 
     acceptProto3 = accept_proto3
+
+    def accept_json_v2(self, data: bytes) -> Call[None]:
+        """``accept(SpanBytesDecoder.JSON_V2.decodeList(data))`` with the decoding on the device
+        (zdl_decode_json_v2), the decoded HBM columns appended to the store as
+        ``accept_proto3`` does. Raises ReferenceIllegalArgumentException where the reference's
+        decoder throws."""
+        if self._json_decoder is None:
+            from .jsonv2 import JsonV2Decoder
+            self._json_decoder = JsonV2Decoder(self._linker.svc, self._linker.ip4, self._linker.ip6, self.device)
+        b = self._json_decoder.decode(data)
+        if b.n_spans:
+            self._evict((self._n_alive + b.n_spans) - self.max_span_count)
+            if self._store is None:
+                self._store = N.Store(self.device)
+            self._store.append_device(b.dev, b.n_spans)
+            self._append_index(b.trace_lo, np.zeros(b.n_spans, np.uint64), b.timestamp)
+        return Call(lambda: None)
+
+    acceptJsonV2 = accept_json_v2
 
     # -- trace selections -------------------------------------------------------------------
     def _storage_order(self, idx):
@@ -290,6 +310,10 @@ class InMemoryStorage:
 
     def close(self):
         self._linker.close()
+        for d in (self._decoder, self._json_decoder):
+            if d is not None:
+                d.close()
+        self._decoder = self._json_decoder = None
         if self._store is not None:
             self._store.close()
             self._store = None
