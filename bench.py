@@ -94,6 +94,49 @@ def proto3_leg(cols, w, S, device, doff, links, reps=5):
             "parity": "same links" if got == exp else "MISMATCH"}
 
 
+def json_v2_leg(cols, w, device, doff, links, reps=3):
+    """Decode the batch's JSON v2 encoding (V2SpanWriter member order, synth.encode_json_v2) on the
+    device, then link the decoded columns with the batch's trace offsets: the links must equal the
+    columnar path's `links` by service name. Device time = the structure passes (block functions,
+    scans, object starts) + k_js_spans, by HIP events; the call time adds the PCIe upload and the
+    trace-id/timestamp download. Compulsory traffic: the bytes once + 52 B/span of columns."""
+    from zipkin_amd import synth
+    from zipkin_amd.columnar import Dictionary
+    from zipkin_amd import _native as N
+    from zipkin_amd.jsonv2 import JsonV2Decoder
+    names = synth.service_names(w)
+    data = synth.encode_json_v2(cols, names).tobytes()
+    dicts = (Dictionary(), Dictionary(), Dictionary())
+    dec = JsonV2Decoder(*dicts, device=device)
+    b = dec.decode(data)  # first pass binds the names
+    ks, ss, cs = [], [], []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        b = dec.decode(data)
+        cs.append(time.perf_counter() - t0)
+        ks.append(dec.kernel_ms())
+        ss.append(dec.struct_ms())
+    km, sm, cm = float(np.median(ks)), float(np.median(ss)), float(np.median(cs)) * 1e3
+    svc = dicts[0]
+    ctx = N.Context(max(len(svc), 1), device=device)
+    dptr = {k: getattr(b.dev, k) for k in ("id", "parent_id", "local_svc", "remote_svc", "local_ip4",
+                                            "local_ip6", "port_flags")}
+    ctx.put_spans_device(dptr, b.n_spans, doff.data_ptr(), cols.n_traces)
+    gp, gc, gn, ge = ctx.link()
+    ctx.close()
+    got = sorted(zip((svc.strings[i] for i in gp.tolist()), (svc.strings[i] for i in gc.tolist()),
+                     gn.tolist(), ge.tolist()))
+    p, c, n, e = links
+    exp = sorted(zip((names[i] for i in p.tolist()), (names[i] for i in c.tolist()), n.tolist(), e.tolist()))
+    dec.close()
+    dev_ms = km + sm
+    algo = len(data) + b.n_spans * 52
+    return {"bytes": len(data), "spans": b.n_spans, "structure_ms": sm, "spans_kernel_ms": km, "device_ms": dev_ms,
+            "call_ms": cm, "spans_per_s": b.n_spans / (dev_ms * 1e-3), "device_gbs": algo / (dev_ms * 1e-3) / 1e9,
+            "roofline_frac": algo / (dev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes": algo,
+            "call_spans_per_s": b.n_spans / (cm * 1e-3), "parity": "same links" if got == exp else "MISMATCH"}
+
+
 def mysql_rows_leg(cols, S, device, max_spans=2_000_000, reps=3):
     """The first traces of the batch (<= max_spans spans) as mysql-v1 cursor rows (one row per
     annotation a span would carry in v1: sr/ca for servers, cs/sa for clients, lc for local spans,
@@ -218,6 +261,7 @@ def main():
     ap.add_argument("--no-h2d", action="store_true", help="skip the host-buffer (PCIe-inclusive) leg")
     ap.add_argument("--no-proto3", action="store_true", help="skip the proto3 ingest side leg")
     ap.add_argument("--no-mysql-rows", action="store_true", help="skip the mysql-v1 rows side leg")
+    ap.add_argument("--no-json", action="store_true", help="skip the JSON v2 ingest side leg")
     ap.add_argument("--inflight", type=int, default=0,
                     help="steps in flight (contexts used round-robin): default 2 at N = 1, 1 at N > 1")
     ap.add_argument("--no-insertion-order", action="store_true",
@@ -380,6 +424,12 @@ def main():
         p3 = proto3_leg(cols, w, S, local, doff, (p, c, n, e))
         log(f"proto3 ingest: kernel {p3['kernel_ms']:.3f} ms ({p3['kernel_gbs']:.0f} GB/s), "
             f"call {p3['call_ms']:.1f} ms, links {p3['parity']}")
+    jleg = None
+    if side and not args.no_json:
+        jleg = json_v2_leg(cols, w, local, doff, (p, c, n, e))
+        log(f"json v2 ingest: {jleg['bytes'] / 1e9:.2f} GB, device {jleg['device_ms']:.2f} ms "
+            f"(structure {jleg['structure_ms']:.2f}, spans {jleg['spans_kernel_ms']:.2f}), "
+            f"call {jleg['call_ms']:.1f} ms, links {jleg['parity']}")
     rows_leg = None
     if side and not args.no_mysql_rows:
         rows_leg = mysql_rows_leg(cols, S, local)
@@ -458,7 +508,7 @@ def main():
                        "step_roofline_frac": bytes_launch / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
                        "k_link_read_frac": read_launch / (tiles * 1e-3) / 1e9 / HBM_PEAK_GBS,
                        "parity": parity, "links": int(len(p)), "insertion_order": ins, "host_buffers": h2d,
-                       "proto3_ingest": p3, "mysql_rows": rows_leg},
+                       "proto3_ingest": p3, "json_v2_ingest": jleg, "mysql_rows": rows_leg},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "k_link", "algorithmic_bytes_per_launch": bytes_launch,

@@ -1,5 +1,5 @@
 """Per-dispatch durations of the named kernels from a rocprofv3 kernel_trace.csv, in launch
-order (tools/gpu_session_tc.sh runs tail_cost.py under the profiler).
+order (run tail_cost.py under rocprofv3 --kernel-trace).
 
     python tools/tail_times.py gpurun_out/tc_x/run_kernel_trace.csv [k_tail] [per_group]
 """

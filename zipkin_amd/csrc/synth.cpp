@@ -438,3 +438,104 @@ extern "C" uint64_t zdl_synth_proto3(uint64_t n, const uint64_t* trace_lo, const
   }
   return pos;
 }
+
+// ---- JSON v2 encoding of synthetic columns (bench / test input for zdl_decode_json_v2) ----
+// V2SpanWriter's member order (internal/V2SpanWriter.java:88-160) for spans [0, n): traceId,
+// parentId, id, kind, name "get", timestamp, duration, localEndpoint {serviceName, ipv4 10.a.b.c
+// from the ipv4 id, port}, remoteEndpoint {serviceName, port 80 when RPORT}, tags {"error":""}
+// when the error flag is set, shared. Returns the byte count; out == NULL only measures.
+namespace {
+struct JW {
+  uint8_t* o;
+  uint64_t pos;
+  void raw(const char* s, size_t n) {
+    if (o) memcpy(o + pos, s, n);
+    pos += n;
+  }
+  void str(const char* s) { raw(s, strlen(s)); }
+  void hex16(uint64_t v) {
+    char b[16];
+    for (int i = 15; i >= 0; --i, v >>= 4) b[i] = "0123456789abcdef"[v & 15];
+    raw(b, 16);
+  }
+  void dec(uint64_t v) {
+    char b[24];
+    int k = 24;
+    do b[--k] = (char)('0' + v % 10), v /= 10;
+    while (v);
+    raw(b + k, 24 - k);
+  }
+};
+}  // namespace
+
+extern "C" uint64_t zdl_synth_json_v2(uint64_t n, const uint64_t* trace_lo, const uint64_t* id,
+                                      const uint64_t* parent_id, const int32_t* local_svc,
+                                      const int32_t* remote_svc, const int32_t* local_ip4,
+                                      const uint32_t* port_flags, const int64_t* timestamp,
+                                      const char* names, const uint32_t* name_off, uint8_t* out) {
+  static const char* kinds[4] = {"CLIENT", "SERVER", "PRODUCER", "CONSUMER"};
+  JW w{out, 0};
+  w.str("[");
+  for (uint64_t i = 0; i < n; ++i) {
+    if (i) w.str(",");
+    w.str("{\"traceId\":\"");
+    w.hex16(trace_lo[i]);
+    w.str("\"");
+    if (parent_id[i] && parent_id[i] != id[i]) {
+      w.str(",\"parentId\":\"");
+      w.hex16(parent_id[i]);
+      w.str("\"");
+    }
+    w.str(",\"id\":\"");
+    w.hex16(id[i]);
+    w.str("\"");
+    const uint32_t pf = port_flags[i];
+    const uint32_t kind = (pf >> 16) & 7;
+    if (kind < 4) {
+      w.str(",\"kind\":\"");
+      w.str(kinds[kind]);
+      w.str("\"");
+    }
+    w.str(",\"name\":\"get\"");
+    if (timestamp[i] > 0) {
+      w.str(",\"timestamp\":");
+      w.dec((uint64_t)timestamp[i]);
+      w.str(",\"duration\":");
+      w.dec(100 + (id[i] % 100000));
+    }
+    for (int side = 0; side < 2; ++side) {
+      const int32_t svc = side ? remote_svc[i] : local_svc[i];
+      const int32_t ip = side ? -1 : local_ip4[i];
+      const uint32_t port = side ? ((pf >> 24 & 1) ? 80u : 0u) : (pf & 0xFFFF);
+      if (svc < 0 && ip < 0 && !port) continue;
+      w.str(side ? ",\"remoteEndpoint\":{" : ",\"localEndpoint\":{");
+      bool any = false;
+      if (svc >= 0) {
+        w.str("\"serviceName\":\"");
+        w.raw(names + name_off[svc], name_off[svc + 1] - name_off[svc]);
+        w.str("\"");
+        any = true;
+      }
+      if (ip >= 0) {
+        w.str(any ? ",\"ipv4\":\"10." : "\"ipv4\":\"10.");
+        w.dec((uint32_t)(ip >> 16) & 255);
+        w.str(".");
+        w.dec((uint32_t)(ip >> 8) & 255);
+        w.str(".");
+        w.dec((uint32_t)ip & 255);
+        w.str("\"");
+        any = true;
+      }
+      if (port) {
+        w.str(any ? ",\"port\":" : "\"port\":");
+        w.dec(port);
+      }
+      w.str("}");
+    }
+    if (pf & (1u << 21)) w.str(",\"tags\":{\"error\":\"\"}");
+    if (((pf >> 19) & 3) == 2) w.str(",\"shared\":true");
+    w.str("}");
+  }
+  w.str("]");
+  return w.pos;
+}

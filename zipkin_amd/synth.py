@@ -146,3 +146,23 @@ def encode_proto3(cols: Columns, names) -> np.ndarray:
     out = np.empty(n, np.uint8)
     L.zdl_synth_proto3(cols.n_spans, *ptrs, out.ctypes.data)
     return out
+
+
+def encode_json_v2(cols: Columns, names) -> np.ndarray:
+    """The spans of `cols` (in column order) as one JSON v2 list (zdl_synth_json_v2 in
+    csrc/synth.cpp, V2SpanWriter's member order). `names[i]` is service i."""
+    L = _synth()
+    if not hasattr(L, "_js"):
+        L.zdl_synth_json_v2.restype = C.c_uint64
+        L.zdl_synth_json_v2.argtypes = [C.c_uint64] + [C.c_void_p] * 11
+        L._js = True
+    blob = "".join(names).encode()
+    off = np.zeros(len(names) + 1, np.uint32)
+    off[1:] = np.cumsum([len(x.encode()) for x in names])
+    args = [cols.trace_lo, cols.id, cols.parent_id, cols.local_svc, cols.remote_svc, cols.local_ip4,
+            cols.port_flags, cols.timestamp]
+    ptrs = [a.ctypes.data for a in args] + [C.c_char_p(blob), off.ctypes.data]
+    n = L.zdl_synth_json_v2(cols.n_spans, *ptrs, None)
+    out = np.empty(n, np.uint8)
+    L.zdl_synth_json_v2(cols.n_spans, *ptrs, out.ctypes.data)
+    return out
