@@ -56,7 +56,7 @@ struct Dict {
 };
 
 template <class Get>
-__host__ __device__ inline uint64_t key_hash(int kind, Get get, uint32_t n) {
+__host__ __device__ __forceinline__ uint64_t key_hash(int kind, Get get, uint32_t n) {
   uint64_t h = 1469598103934665603ull ^ (uint64_t)(kind + 1);
   h *= 1099511628211ull;
   for (uint32_t i = 0; i < n; ++i) {
@@ -559,8 +559,9 @@ struct zdl_decoder {
   float kernel_ms = 0.f;
   int fmt = 0;  // the resident batch: 0 proto3, 1 JSON v2
   // JSON v2 structure (zdl_json.inc)
-  DBuf<int4> js_fn, js_gfn;
-  DBuf<unsigned long long> js_gst, js_misc;  // misc: [0] E (the array's closing bracket), [1] spans before E
+  DBuf<int4> js_fn, js_gfn, js_lpre;  // block functions / prefixes, group functions, lane prefixes
+  DBuf<uint16_t> js_slots;           // per block: its objects' block-relative positions
+  DBuf<unsigned long long> js_gst, js_misc;  // misc: [0] E (the array's closing bracket), [1] spans before E, [2] lane overflow
   DBuf<uint32_t> js_cnt;
   DBuf<uint64_t> js_off, js_starts;
   DBuf<uint8_t> js_tmp;  // hipCUB scan scratch
@@ -857,39 +858,55 @@ int zdl_decode_json_v2(zdl_decoder* d, const uint8_t* data, uint64_t len, zdl_de
   const hipStream_t s = d->stream;
   const uint32_t nblk = (uint32_t)((len + kBlk - 1) / kBlk);
   const uint32_t ngroup = (nblk + kGroup - 1) / kGroup;
-  DEC_TRY(d, d->buf.ensure(len));
+  DEC_TRY(d, d->buf.ensure(len + 64));  // k_js_spans reads whole aligned 16-byte chunks
   DEC_TRY(d, hipMemcpyAsync(d->buf.p, data, len, hipMemcpyHostToDevice, s));
   DEC_TRY(d, d->js_fn.ensure(nblk));
+  DEC_TRY(d, d->js_lpre.ensure((size_t)nblk * 64));
   DEC_TRY(d, d->js_gfn.ensure(ngroup));
   DEC_TRY(d, d->js_gst.ensure(ngroup));
   DEC_TRY(d, d->js_cnt.ensure(nblk));
   DEC_TRY(d, d->js_off.ensure(nblk));
-  DEC_TRY(d, d->js_misc.ensure(2));
-  DEC_TRY(d, d->js_h.ensure(2));
+  DEC_TRY(d, d->js_slots.ensure((size_t)nblk * kBlockCap));
+  DEC_TRY(d, d->js_misc.ensure(3));
+  DEC_TRY(d, d->js_h.ensure(3));
   size_t tmp = 0;
   DEC_TRY(d, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, d->js_cnt.p, d->js_off.p, (int)nblk, s));
   DEC_TRY(d, d->js_tmp.ensure(tmp));
   DEC_TRY(d, hipEventRecord(d->ev_s[0], s));
-  DEC_TRY(d, hipMemsetAsync(d->js_misc.p, 0xFF, 8, s));
-  DEC_TRY(d, hipMemsetAsync(d->js_misc.p + 1, 0, 8, s));
+  DEC_TRY(d, hipMemsetAsync(d->js_misc.p, 0xFF, 8, s));     // E
+  DEC_TRY(d, hipMemsetAsync(d->js_misc.p + 1, 0, 16, s));   // spans before E, lane overflow
   const unsigned g4 = (unsigned)((nblk + 3) / 4);
-  k_js_fn<<<g4, 256, 0, s>>>(d->buf.p, len, nblk, d->js_fn.p);
+  k_js_fn<<<g4, 256, 0, s>>>(d->buf.p, len, nblk, d->js_fn.p, d->js_lpre.p);
   k_js_group<<<ngroup, 1024, 0, s>>>(d->js_fn.p, nblk, d->js_gfn.p);
   k_js_top<<<1, 1024, 0, s>>>(d->js_gfn.p, ngroup, d->js_gst.p);
-  k_js_starts<0><<<g4, 256, 0, s>>>(d->buf.p, len, nblk, d->js_fn.p, d->js_gst.p, d->js_cnt.p, nullptr, nullptr,
-                                     d->js_misc.p);
+  uint32_t* over = (uint32_t*)(d->js_misc.p + 2);
+  k_js_starts<<<g4, 256, 0, s>>>(d->buf.p, len, nblk, d->js_fn.p, d->js_lpre.p, d->js_gst.p, d->js_cnt.p,
+                                  d->js_slots.p, over, d->js_misc.p);
   DEC_TRY(d, hipGetLastError());
   DEC_TRY(d, hipcub::DeviceScan::ExclusiveSum(d->js_tmp.p, tmp, d->js_cnt.p, d->js_off.p, (int)nblk, s));
   uint64_t last_off = 0;
-  uint32_t last_cnt = 0;
+  uint32_t last_cnt = 0, over_h = 0;
   DEC_TRY(d, hipMemcpyAsync(&last_off, d->js_off.p + nblk - 1, 8, hipMemcpyDeviceToHost, s));
   DEC_TRY(d, hipMemcpyAsync(&last_cnt, d->js_cnt.p + nblk - 1, 4, hipMemcpyDeviceToHost, s));
+  DEC_TRY(d, hipMemcpyAsync(&over_h, over, 4, hipMemcpyDeviceToHost, s));
   DEC_TRY(d, hipStreamSynchronize(s));
+  if (over_h) {  // some lane held more than kLaneCap objects: the exact two-pass path
+    k_js_starts_exact<0><<<g4, 256, 0, s>>>(d->buf.p, len, nblk, d->js_fn.p, d->js_lpre.p, d->js_gst.p, d->js_cnt.p,
+                                             nullptr, nullptr);
+    DEC_TRY(d, hipGetLastError());
+    DEC_TRY(d, hipcub::DeviceScan::ExclusiveSum(d->js_tmp.p, tmp, d->js_cnt.p, d->js_off.p, (int)nblk, s));
+    DEC_TRY(d, hipMemcpyAsync(&last_off, d->js_off.p + nblk - 1, 8, hipMemcpyDeviceToHost, s));
+    DEC_TRY(d, hipMemcpyAsync(&last_cnt, d->js_cnt.p + nblk - 1, 4, hipMemcpyDeviceToHost, s));
+    DEC_TRY(d, hipStreamSynchronize(s));
+  }
   const uint64_t total = last_off + last_cnt;
   if (total) {
     DEC_TRY(d, d->js_starts.ensure(total));
-    k_js_starts<1><<<g4, 256, 0, s>>>(d->buf.p, len, nblk, d->js_fn.p, d->js_gst.p, nullptr, d->js_off.p,
-                                       d->js_starts.p, d->js_misc.p);
+    if (over_h)
+      k_js_starts_exact<1><<<g4, 256, 0, s>>>(d->buf.p, len, nblk, d->js_fn.p, d->js_lpre.p, d->js_gst.p, nullptr,
+                                               d->js_off.p, d->js_starts.p);
+    else
+      k_js_gather<<<g4, 256, 0, s>>>(d->js_slots.p, d->js_cnt.p, d->js_off.p, nblk, d->js_starts.p);
     k_js_before<<<(unsigned)((total + 255) / 256), 256, 0, s>>>(d->js_starts.p, total, d->js_misc.p, d->js_misc.p + 1);
     DEC_TRY(d, hipGetLastError());
   }
