@@ -254,6 +254,50 @@ def test_comm_job_of_one_rank(config):
     assert got == again == sorted(_oracle(cols))
 
 
+def _c5_like(traces=100_000):
+    return synth.Workload("c5_like_10k", 0x5EED0078, traces, 10_000, max_depth=32, size_dist=1, pareto_alpha=1.3,
+                          max_size=3000, max_fanout=200, zipf_s=1.1)
+
+
+@pytest.mark.parametrize("forced", [False, True])
+def test_device_group_sparse_lists_combined(forced, monkeypatch):
+    """Device groups above 1024 services keep a sparse list per device; zdl_link sends every
+    device's list to the first (ncclSend/ncclRecv) and sums them per cell there (sparse_add:
+    DependencyLinker.merge). On the box's one device, and forced (ZDL_SPARSE=1) at C4's size."""
+    if forced:
+        monkeypatch.setenv("ZDL_SPARSE", "1")
+    w = synth.C4.scaled(100_000) if forced else _c5_like()
+    cols = synth.generate(w)
+    g = N.Context(w.total_services, device_ids=[0])
+    g.put_spans(cols)
+    g.put_spans(cols)
+    got = sorted(_tuples(*g.link()))
+    g.reset()
+    g.put_spans(cols)
+    once = sorted(_tuples(*g.link()))
+    g.close()
+    exp = sorted(_oracle(cols))
+    assert once == exp
+    assert got == [(a, b, 2 * n, 2 * e) for a, b, n, e in exp]
+
+
+def test_comm_job_of_one_rank_sparse():
+    """A sparse context joined to a one-rank job: zdl_link exchanges list lengths
+    (ncclAllGather) and lists (ncclSend/ncclRecv) and sums them (comm_sum_sparse)."""
+    w = _c5_like()
+    cols = synth.generate(w)
+    ctx = N.Context(w.total_services)
+    ctx.comm_init(N.Context.comm_unique_id(), 0, 1)
+    ctx.put_spans(cols)
+    got = sorted(_tuples(*ctx.link()))
+    ctx.put_spans(cols)
+    twice = sorted(_tuples(*ctx.link()))
+    ctx.close()
+    exp = sorted(_oracle(cols))
+    assert got == exp
+    assert twice == [(a, b, 2 * n, 2 * e) for a, b, n, e in exp]
+
+
 @pytest.mark.parametrize("exact", [False, True])
 def test_c5_body_big_trace_paths_vs_cpp(exact, monkeypatch):
     """Traces above 64 spans: the sort-free path for simple ids (big_simple, LDS-resident up

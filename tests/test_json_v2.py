@@ -405,6 +405,11 @@ def test_gpu_decode_edge_inputs():
         with pytest.raises(N.ReferenceIllegalArgumentException):
             dec.decode(data)
     assert dec.decode(b"[" + b",".join([one] * 3) + b"] trailing {[").n_spans == 3
+    # more than 4 objects in one 64-byte lane (only "{}"-dense input): the exact starts path
+    with pytest.raises(N.ReferenceIllegalArgumentException):
+        dec.decode(b"[" + b",".join([b"{}"] * 200) + b"]")
+    tight = b'{"traceId":1,"id":2}'  # the shortest span objects: 4 starts in some lanes
+    assert dec.decode(b"[" + b",".join([tight] * 500) + b"]").n_spans == 500
     deep = b"[" + one[:-1] + b',"x":' + b"[" * 70 + b"]" * 70 + b"}]"
     with pytest.raises(N.ZdlError) as ei:
         dec.decode(deep)

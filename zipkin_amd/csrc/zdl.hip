@@ -1350,6 +1350,12 @@ struct zdl_ctx {
   ncclComm_t comm = nullptr;
   int comm_rank = 0, comm_world = 1;
   DevBuf<unsigned long long> red_call, red_err;  // the summed tables
+  // sparse combine (device groups / jobs above 1024 services): every device's or rank's sorted
+  // list gathered here (cell, call, err), summed into gacc (sparse_add: DependencyLinker.merge)
+  DevBuf<uint32_t> gx_cell;
+  DevBuf<unsigned long long> gx_call, gx_err;
+  DevBuf<uint64_t> gx_n;  // ranks' list lengths (ncclAllGather)
+  SparseTable gacc;
   DevBuf<unsigned long long> prof;
   int prof_on = 0;
   DevBuf<uint64_t> b_id, b_pid;
@@ -1646,6 +1652,7 @@ void zdl_destroy(zdl_ctx* c) {
   c->lg_start.release();
   c->tr_node.release(); c->tr_parent.release(); c->tr_bfs.release();
   c->acc.release(); c->sw.release(); c->seg_src.release(); c->seg_n.release(); c->seg_off.release();
+  c->gx_cell.release(); c->gx_call.release(); c->gx_err.release(); c->gx_n.release(); c->gacc.release();
   c->tseg_big.release(); c->tseg_win.release(); c->lin.release(); c->seg_tmp.release();
   c->b_id.release(); c->b_pid.release(); c->b_lsvc.release(); c->b_rsvc.release(); c->b_ip4.release();
   c->b_ip6.release(); c->b_parent.release(); c->b_pf.release(); c->b_perm.release(); c->b_live.release();
@@ -2575,12 +2582,13 @@ static int ensure_rec(zdl_ctx* c, uint64_t m) {
 }
 
 // A sparse context's links: its sorted list (cell = id order), rank-sorted when ranks are set.
-static int link_sparse(zdl_ctx* c, zdl_links* out) {
-  const uint64_t m = c->acc.n;
+static int link_sparse(zdl_ctx* c, zdl_links* out, const SparseTable* tab = nullptr) {
+  const SparseTable& t = tab ? *tab : c->acc;
+  const uint64_t m = t.n;
   int rc = ensure_rec(c, m);
   if (rc != ZDL_OK) return rc;
   const size_t cap = c->h_rec_cap;
-  HIP_TRY(c, compact_sparse(c->lw, c->acc.cell, c->acc.call, c->acc.err, m, c->S,
+  HIP_TRY(c, compact_sparse(c->lw, t.cell, t.call, t.err, m, c->S,
                             c->nrank[0] ? c->rank[0].p : nullptr, c->nrank[0], (int32_t*)c->d_rec,
                             (int32_t*)(c->d_rec + 4 * cap), (int64_t*)(c->d_rec + 8 * cap),
                             (int64_t*)(c->d_rec + 16 * cap), c->stream));
@@ -2596,6 +2604,7 @@ static int link_sparse(zdl_ctx* c, zdl_links* out) {
   return ZDL_OK;
 }
 static int group_link(zdl_ctx* g, int order, zdl_links* out);
+static int comm_sum_sparse(zdl_ctx* c);  // multi-process job, sparse lists (below)
 
 extern "C" {
 
@@ -2611,6 +2620,11 @@ int zdl_link(zdl_ctx* c, int order, zdl_links* out) {
   }
   if (order != ZDL_ORDER_SORTED) return fail(c, ZDL_EINVAL, "zdl_link: order must be ZDL_ORDER_SORTED or ZDL_ORDER_INSERTION");
   HIP_TRY(c, enter(c));
+  if (c->sparse && c->comm) {  // a rank of a multi-process job: every rank's list, summed
+    const int rc = comm_sum_sparse(c);
+    if (rc != ZDL_OK) return rc;
+    return link_sparse(c, out, &c->gacc);
+  }
   if (c->sparse) return link_sparse(c, out);
   if (c->comm) {  // a rank of a multi-process job: the links of every rank's tables
     const int rc = comm_sum_tables(c);
@@ -2941,7 +2955,8 @@ static zdl_ctx* create_group(const zdl_config* cfg) {
     one.device = cfg->device_ids[d];
     one.n_devices = 0;
     one.device_ids = nullptr;
-    one.flags |= ZDL_FLAG_DENSE_TABLE;  // the RCCL reduce sums S x S tables
+    // above 1024 services every device keeps a sparse list (ZDL_FLAG_DENSE_TABLE keeps tables):
+    // zdl_link gathers the lists onto the first device and sums them (group_link_sparse)
     zdl_ctx* s = zdl_create(&one);
     if (!s) {
       const std::string e = g_create_error;
@@ -3048,6 +3063,53 @@ static int group_reduce(zdl_ctx* g, unsigned long long* rcall, unsigned long lon
   return ZDL_OK;
 }
 
+// Device groups above 1024 services: every device's sorted list sent to the first device
+// (ncclSend / ncclRecv over xGMI, exact lengths), concatenated and summed per cell there
+// (sparse_add: radix sort, reduce by key - DependencyLinker.merge, DependencyLinker.java:189-204).
+// an allgather of compacted (pair, call, err) instead of S x S tables.
+static int group_link_sparse(zdl_ctx* g, zdl_links* out) {
+  zdl_ctx* s0 = g->sub[0];
+  const size_t N = g->sub.size();
+  std::vector<uint64_t> n(N), at(N + 1, 0);
+  for (size_t d = 0; d < N; ++d) {
+    n[d] = g->sub[d]->acc.n;
+    at[d + 1] = at[d] + n[d];
+  }
+  const uint64_t total = at[N];
+  HIP_TRY(g, enter(s0));
+  HIP_TRY(g, s0->gx_cell.ensure(total));
+  HIP_TRY(g, s0->gx_call.ensure(total));
+  HIP_TRY(g, s0->gx_err.ensure(total));
+  ncclResult_t r = ncclGroupStart();
+  for (size_t d = 1; d < N && r == ncclSuccess; ++d) {
+    zdl_ctx* s = g->sub[d];
+    if (!n[d]) continue;
+    (void)hipSetDevice(s->device);
+    r = ncclSend(s->acc.cell, n[d], ncclUint32, 0, g->comms[d], s->stream);
+    if (r == ncclSuccess) r = ncclSend(s->acc.call, n[d], ncclUint64, 0, g->comms[d], s->stream);
+    if (r == ncclSuccess) r = ncclSend(s->acc.err, n[d], ncclUint64, 0, g->comms[d], s->stream);
+    (void)hipSetDevice(s0->device);
+    if (r == ncclSuccess) r = ncclRecv(s0->gx_cell.p + at[d], n[d], ncclUint32, (int)d, g->comms[0], s0->stream);
+    if (r == ncclSuccess) r = ncclRecv(s0->gx_call.p + at[d], n[d], ncclUint64, (int)d, g->comms[0], s0->stream);
+    if (r == ncclSuccess) r = ncclRecv(s0->gx_err.p + at[d], n[d], ncclUint64, (int)d, g->comms[0], s0->stream);
+  }
+  const ncclResult_t r2 = ncclGroupEnd();
+  (void)hipSetDevice(s0->device);
+  if (r != ncclSuccess || r2 != ncclSuccess)
+    return fail(g, ZDL_EDEVICE, std::string("device group: ncclSend/Recv: ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
+  hipStream_t st = s0->stream;
+  if (n[0]) {
+    HIP_TRY(g, hipMemcpyAsync(s0->gx_cell.p, s0->acc.cell, n[0] * 4, hipMemcpyDeviceToDevice, st));
+    HIP_TRY(g, hipMemcpyAsync(s0->gx_call.p, s0->acc.call, n[0] * 8, hipMemcpyDeviceToDevice, st));
+    HIP_TRY(g, hipMemcpyAsync(s0->gx_err.p, s0->acc.err, n[0] * 8, hipMemcpyDeviceToDevice, st));
+  }
+  s0->gacc.n = 0;
+  int kb = 1;
+  while ((1ull << kb) < (uint64_t)g->S * g->S) ++kb;
+  HIP_TRY(g, sparse_add(s0->sw, s0->gacc, s0->gx_cell.p, s0->gx_call.p, s0->gx_err.p, total, kb, st));
+  return group_first(g, link_sparse(s0, out, &s0->gacc));
+}
+
 static int group_link(zdl_ctx* g, int order, zdl_links* out) {
   if (order != ZDL_ORDER_SORTED) return fail(g, ZDL_EINVAL, "device group: zdl_link returns ZDL_ORDER_SORTED");
   zdl_ctx* s0 = g->sub[0];
@@ -3055,6 +3117,7 @@ static int group_link(zdl_ctx* g, int order, zdl_links* out) {
     const int rc = zdl_sync(g->sub[d]);
     if (rc != ZDL_OK) return group_first(g, rc, g->sub[d]);
   }
+  if (s0->sparse) return group_link_sparse(g, out);
   HIP_TRY(g, enter(s0));
   const size_t SS = (size_t)g->S * g->S;
   HIP_TRY(g, s0->red_call.ensure(SS));
@@ -3065,6 +3128,7 @@ static int group_link(zdl_ctx* g, int order, zdl_links* out) {
 }
 
 int group_export(zdl_ctx* g, void* dev_call, void* dev_err) {
+  if (g->sub[0]->sparse) return fail(g, ZDL_EINVAL, "zdl_table_export: a sparse device group has no S x S table");
   HIP_TRY(g, enter(g->sub[0]));
   return group_reduce(g, (unsigned long long*)dev_call, (unsigned long long*)dev_err);
 }
@@ -3082,6 +3146,53 @@ static int comm_sum_tables(zdl_ctx* c) {
   return ZDL_OK;
 }
 
+// Multi-process jobs above 1024 services: the ranks' list lengths by ncclAllGather, then every
+// rank's list to every rank (ncclSend / ncclRecv, exact lengths: an all-gather of unequal
+// parts), summed per cell on each rank (sparse_add) - every rank returns the job's links.
+static int comm_sum_sparse(zdl_ctx* c) {
+  const int W = c->comm_world, me = c->comm_rank;
+  hipStream_t st = c->stream;
+  HIP_TRY(c, c->gx_n.ensure((size_t)W + 1));
+  HIP_TRY(c, hipMemcpyAsync(c->gx_n.p + W, &c->acc.n, 8, hipMemcpyHostToDevice, st));
+  ncclResult_t r = ncclAllGather(c->gx_n.p + W, c->gx_n.p, 1, ncclUint64, c->comm, st);
+  if (r != ncclSuccess) return fail(c, ZDL_EDEVICE, std::string("ncclAllGather: ") + ncclGetErrorString(r));
+  std::vector<uint64_t> n(W), at(W + 1, 0);
+  HIP_TRY(c, hipMemcpyAsync(n.data(), c->gx_n.p, 8 * (size_t)W, hipMemcpyDeviceToHost, st));
+  HIP_TRY(c, hipStreamSynchronize(st));
+  for (int k = 0; k < W; ++k) at[k + 1] = at[k] + n[k];
+  const uint64_t total = at[W];
+  HIP_TRY(c, c->gx_cell.ensure(total));
+  HIP_TRY(c, c->gx_call.ensure(total));
+  HIP_TRY(c, c->gx_err.ensure(total));
+  r = ncclGroupStart();
+  for (int k = 0; k < W && r == ncclSuccess; ++k) {
+    if (k == me) continue;
+    if (n[me]) {
+      r = ncclSend(c->acc.cell, n[me], ncclUint32, k, c->comm, st);
+      if (r == ncclSuccess) r = ncclSend(c->acc.call, n[me], ncclUint64, k, c->comm, st);
+      if (r == ncclSuccess) r = ncclSend(c->acc.err, n[me], ncclUint64, k, c->comm, st);
+    }
+    if (r == ncclSuccess && n[k]) {
+      r = ncclRecv(c->gx_cell.p + at[k], n[k], ncclUint32, k, c->comm, st);
+      if (r == ncclSuccess) r = ncclRecv(c->gx_call.p + at[k], n[k], ncclUint64, k, c->comm, st);
+      if (r == ncclSuccess) r = ncclRecv(c->gx_err.p + at[k], n[k], ncclUint64, k, c->comm, st);
+    }
+  }
+  const ncclResult_t r2 = ncclGroupEnd();
+  if (r != ncclSuccess || r2 != ncclSuccess)
+    return fail(c, ZDL_EDEVICE, std::string("ncclSend/Recv: ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
+  if (n[me]) {
+    HIP_TRY(c, hipMemcpyAsync(c->gx_cell.p + at[me], c->acc.cell, n[me] * 4, hipMemcpyDeviceToDevice, st));
+    HIP_TRY(c, hipMemcpyAsync(c->gx_call.p + at[me], c->acc.call, n[me] * 8, hipMemcpyDeviceToDevice, st));
+    HIP_TRY(c, hipMemcpyAsync(c->gx_err.p + at[me], c->acc.err, n[me] * 8, hipMemcpyDeviceToDevice, st));
+  }
+  c->gacc.n = 0;
+  int kb = 1;
+  while ((1ull << kb) < (uint64_t)c->S * c->S) ++kb;
+  HIP_TRY(c, sparse_add(c->sw, c->gacc, c->gx_cell.p, c->gx_call.p, c->gx_err.p, total, kb, st));
+  return ZDL_OK;
+}
+
 extern "C" {
 
 int zdl_comm_unique_id(uint8_t* out) {
@@ -3096,7 +3207,6 @@ int zdl_comm_init(zdl_ctx* c, const uint8_t* id, int rank, int world) {
   if (!c || !id || world < 1 || rank < 0 || rank >= world) return fail(c, ZDL_EINVAL, "zdl_comm_init: bad rank / world");
   if (!c->sub.empty()) return fail(c, ZDL_EINVAL, "zdl_comm_init: a device group has its own communicator");
   if (c->ord || c->days) return fail(c, ZDL_EINVAL, "zdl_comm_init: insertion order and daily buckets are per process");
-  if (c->sparse) return fail(c, ZDL_EINVAL, "zdl_comm_init: create the context with ZDL_FLAG_DENSE_TABLE (RCCL sums S x S tables)");
   if (c->comm) return fail(c, ZDL_EINVAL, "zdl_comm_init: already joined");
   HIP_TRY(c, enter(c));
   ncclUniqueId u;
