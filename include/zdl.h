@@ -45,6 +45,8 @@ extern "C" {
 #define ZDL_EDEVICE    (-3)  /* HIP runtime error */
 #define ZDL_EREF_NPE   (-4)  /* the reference throws NullPointerException for this input (quirk Q1) */
 #define ZDL_EREF_IAE   (-5)  /* the reference throws IllegalArgumentException for this input */
+#define ZDL_EREF_NSE   (-6)  /* the reference throws NoSuchElementException (an eviction that
+                                empties the store, InMemoryStorage.java:184-196) */
 
 /* ---- port_flags column bit layout (one u32 per span) ---- */
 #define ZDL_PF_PORT_MASK     0x0000FFFFu /* local endpoint port, 0 = null (Endpoint.java:245-260) */
@@ -189,22 +191,53 @@ int zdl_put_spans_device(zdl_ctx* ctx, const zdl_span_cols* dev_cols, uint64_t n
 /* ---- device-resident span store (the ingest side of InMemoryStorage,
  * storage/InMemoryStorage.java:156-181 accept) ----
  * Spans are appended to HBM columns once (zdl_store_append copies the borrowed columns, host
- * or device memory, e.g. a zdl_decoded's; `timestamp` may be NULL = absent). A getDependencies-style query then uploads only
- * its selection: zdl_put_stored links the stored spans perm[0..n_sel) as CSR-grouped traces
- * (trace t = positions [trace_offsets[t], trace_offsets[t+1]) of perm, storage order), like
- * zdl_put_spans would on the gathered columns. Synchronous. The store may serve any context
- * of its device; eviction is the caller's (a selection simply leaves spans out). */
+ * or device memory, e.g. a zdl_decoded's; `timestamp` may be NULL = absent, `trace_lo` NULL =
+ * 0). Each stored span also keeps its trace id (low and high 64 bits; high 0 for a 64-bit id)
+ * and an alive byte, from which the store answers InMemoryStorage's questions on the device:
+ * eviction (zdl_store_evict) and the trace selection of a query (zdl_store_select), which
+ * zdl_put_selection gathers and links without leaving HBM. Positions count appends (0..size);
+ * evicted spans keep theirs until zdl_store_compact_evicted / zdl_store_compact renumber. */
 typedef struct zdl_store zdl_store;
 zdl_store*  zdl_store_create(int device);
 void        zdl_store_destroy(zdl_store* store);
 const char* zdl_store_last_error(const zdl_store* store);
 int         zdl_store_append(zdl_store* store, const zdl_span_cols* cols, uint64_t n_spans);
+/* zdl_store_append with the high 64 bits of each span's trace id (NULL = all 0). */
+int         zdl_store_append_traced(zdl_store* store, const zdl_span_cols* cols, const uint64_t* trace_hi,
+                                    uint64_t n_spans);
 int         zdl_store_clear(zdl_store* store);
 /* Keeps the stored spans keep[0..n_keep) (ascending positions), in that order, and frees the
- * rest: what InMemoryStorage's deleteOldestTrace releases (InMemoryStorage.java:193-211), in
- * one device gather once evicted spans pile up. Positions are renumbered 0..n_keep). */
+ * rest, in one device gather. Positions are renumbered 0..n_keep). */
 int         zdl_store_compact(zdl_store* store, const uint32_t* keep, uint64_t n_keep);
-uint64_t    zdl_store_size(const zdl_store* store);
+/* Frees the evicted spans (what deleteOldestTrace releases, InMemoryStorage.java:193-211) in
+ * one device gather; the alive spans keep their order and are renumbered. */
+int         zdl_store_compact_evicted(zdl_store* store);
+uint64_t    zdl_store_size(const zdl_store* store);   /* stored positions, evicted included */
+uint64_t    zdl_store_alive(const zdl_store* store);  /* spans not evicted */
+/* evictToRecoverSpans(to_recover) (InMemoryStorage.java:184-211): deleteOldestTrace - every
+ * span of the low trace id whose smallest (timestamp, lowTraceId) key is the smallest - until
+ * at least to_recover spans are gone; *evicted = their number. ZDL_EREF_NSE when the store
+ * runs empty first (everything is evicted, as the reference's loop does before it throws). */
+int         zdl_store_evict(zdl_store* store, uint64_t to_recover, uint64_t* evicted);
+/* Trace selections of the alive spans, each trace in IMS storage order (spansByTraceId,
+ * InMemoryStorage.java:448-454: distinct (lowTraceId, timestamp) keys in first-seen order,
+ * then arrival): */
+#define ZDL_SELECT_NEWEST     0  /* getDependencies(endTs, lookback) / getTraces(request): low
+                                    trace ids by their newest timestamp, then lowTraceId, both
+                                    descending (TIMESTAMP_DESCENDING, :272-291, 356-366) */
+#define ZDL_SELECT_ALL        1  /* getTraces() (:251-262): low trace ids ascending */
+#define ZDL_SELECT_ALL_STRICT 2  /* getTraces() with strictTraceId: each low trace id split by
+                                    the full trace id, first-seen order (:241-249) */
+/* Computes the selection on the device (kept by the store until the next change);
+ * *n_sel spans in *n_traces traces. */
+int         zdl_store_select(zdl_store* store, int mode, uint64_t* n_sel, uint64_t* n_traces);
+/* Copies the current selection out: perm[0..n_sel) positions, trace_offsets[0..n_traces]. */
+int         zdl_store_selection(const zdl_store* store, uint32_t* perm, uint64_t* trace_offsets);
+/* Links the store's current selection (zdl_put_stored without the upload). Synchronous. */
+int         zdl_put_selection(zdl_ctx* ctx, const zdl_store* store);
+/* Links the stored spans perm[0..n_sel) (host) as CSR-grouped traces (trace t = positions
+ * [trace_offsets[t], trace_offsets[t+1]) of perm, storage order), like zdl_put_spans would on
+ * the gathered columns. Synchronous. The store may serve any context of its device. */
 int zdl_put_stored(zdl_ctx* ctx, const zdl_store* store, const uint32_t* perm, uint64_t n_sel,
                    const uint64_t* trace_offsets, uint64_t n_traces);
 

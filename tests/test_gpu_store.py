@@ -139,3 +139,77 @@ def test_get_dependencies_snapshots_its_traces():
     store.clear()
     assert _as_list(call.execute()) == _as_list(ref.get_dependencies(end_ms, 86_400_000 * 2))
     store.close()
+
+
+def _index_cols(r, n, n_lo, n_ts):
+    """n spans over n_lo low trace ids (some with two high ids), n_ts distinct timestamps
+    (0 = absent among them): heavy ties for every ordering key."""
+    from zipkin_amd.columnar import Columns
+    lows = r.integers(1, 2 ** 63, n_lo, dtype=np.uint64)
+    lo = lows[r.integers(0, n_lo, n)]
+    hi = np.where(r.random(n) < 0.3, r.integers(1, 3, n, dtype=np.uint64), np.uint64(0))
+    ts = r.integers(0, n_ts, n).astype(np.int64) * 1000
+    z32 = np.zeros(n, np.int32)
+    cols = Columns(lo, r.integers(1, 2 ** 63, n, dtype=np.uint64), np.zeros(n, np.uint64), z32, z32 - 1,
+                   z32 - 1, z32 - 1, np.zeros(n, np.uint32), ts, np.zeros(1, np.uint64))
+    return cols, lo, hi, ts
+
+
+@pytest.mark.parametrize("seed,n,n_lo,n_ts", [(0, 2000, 50, 5), (1, 50_000, 3000, 40), (2, 400_000, 9000, 1000),
+                                              (3, 30_000, 1, 7), (4, 30_000, 30_000, 3)])
+def test_store_index_vs_numpy_restatement(seed, n, n_lo, n_ts):
+    """zdl_store_evict / zdl_store_select against oracle/ims_index.py position for position,
+    over appends, evictions and compactions (which renumber the store)."""
+    from oracle import ims_index as X
+    r = np.random.default_rng(seed)
+    st = N.Store(0)
+    lo = np.zeros(0, np.uint64)
+    hi = np.zeros(0, np.uint64)
+    ts = np.zeros(0, np.int64)
+    alive = np.zeros(0, bool)
+    for step in range(4):
+        cols, l, h, t = _index_cols(r, n // 4, n_lo, n_ts)
+        if step:
+            want = int(r.integers(1, max(2, alive.sum() // 3)))
+            alive, ev, exhausted = X.evict(lo, ts, alive, want)
+            assert st.evict(want) == ev and not exhausted
+            assert st.alive == int(alive.sum())
+        if step == 2:  # release the evicted spans: both sides renumber
+            st.compact_evicted()
+            keep = np.nonzero(alive)[0]
+            lo, hi, ts, alive = lo[keep], hi[keep], ts[keep], alive[keep]
+            assert len(st) == len(keep)
+        st.append(cols, h)
+        lo, hi, ts = np.concatenate([lo, l]), np.concatenate([hi, h]), np.concatenate([ts, t])
+        alive = np.concatenate([alive, np.ones(len(l), bool)])
+        for mode in (X.SELECT_NEWEST, X.SELECT_ALL, X.SELECT_ALL_STRICT):
+            perm, off = st.selection(mode)
+            want_perm, want_off = X.select(lo, hi, ts, alive, mode)
+            np.testing.assert_array_equal(off, want_off)
+            np.testing.assert_array_equal(perm, want_perm)
+    with pytest.raises(N.ZdlError) as e:  # more than the store holds: everything goes, then NSE
+        st.evict(st.alive + 1)
+    assert e.value.code == N.ZDL_EREF_NSE and st.alive == 0
+    assert st.selection(X.SELECT_NEWEST)[0].size == 0
+    st.close()
+
+
+def test_store_index_link_matches_host_selection():
+    """zdl_put_selection (device-resident selection) links what zdl_put_stored links for the
+    same selection uploaded from the host."""
+    from oracle import ims_index as X
+    from zipkin_amd import synth
+    w = synth.C2.scaled(50_000)
+    cols = synth.generate(w)
+    st = N.Store(0)
+    st.append(cols)
+    for mode in (X.SELECT_NEWEST, X.SELECT_ALL):
+        perm, off = st.selection(mode)
+        ctx = N.Context(w.total_services, insertion_order=True)
+        ctx.put_selection(st)
+        got = [a.tolist() for a in ctx.link(order=N.ZDL_ORDER_INSERTION)]
+        ctx.reset()
+        ctx.put_stored(st, perm, off)
+        assert got == [a.tolist() for a in ctx.link(order=N.ZDL_ORDER_INSERTION)]
+        ctx.close()
+    st.close()

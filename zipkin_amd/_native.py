@@ -11,7 +11,8 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ZDL_LIB_PATH") or os.path.join(HERE, "libzdl.so")  # override: A/B builds
 
-ZDL_OK, ZDL_EINVAL, ZDL_ENOMEM, ZDL_EDEVICE, ZDL_EREF_NPE, ZDL_EREF_IAE = 0, -1, -2, -3, -4, -5
+ZDL_OK, ZDL_EINVAL, ZDL_ENOMEM, ZDL_EDEVICE, ZDL_EREF_NPE, ZDL_EREF_IAE, ZDL_EREF_NSE = 0, -1, -2, -3, -4, -5, -6
+ZDL_SELECT_NEWEST, ZDL_SELECT_ALL, ZDL_SELECT_ALL_STRICT = 0, 1, 2
 ZDL_DICT_SERVICE, ZDL_DICT_IPV4, ZDL_DICT_IPV6 = 0, 1, 2
 # JSON v2 keys (include/zdl.h): raw service token text, ipv4 text, ipv6 text (missing list only)
 ZDL_DICT_JSON_SERVICE, ZDL_DICT_JSON_IPV4, ZDL_DICT_JSON_IPV6TEXT = 3, 4, 5
@@ -37,7 +38,8 @@ EXPORTS = (
     "zdl_link", "zdl_merge_links", "zdl_add_links", "zdl_reset", "zdl_table_export",
     "zdl_table_import", "zdl_get_kernel_times", "zdl_stream", "zdl_set_days", "zdl_link_days",
     "zdl_store_create", "zdl_store_destroy", "zdl_store_last_error", "zdl_store_append", "zdl_store_clear",
-    "zdl_store_size", "zdl_put_stored", "zdl_store_compact",
+    "zdl_store_size", "zdl_put_stored", "zdl_store_compact", "zdl_store_append_traced", "zdl_store_alive",
+    "zdl_store_evict", "zdl_store_compact_evicted", "zdl_store_select", "zdl_store_selection", "zdl_put_selection",
     "zdl_decoder_create", "zdl_decoder_destroy", "zdl_decoder_last_error", "zdl_decoder_bind",
     "zdl_decoder_dict_size", "zdl_decoder_missing", "zdl_decode_proto3", "zdl_decode_proto3_retry",
     "zdl_decoder_download", "zdl_decoder_kernel_ms", "zdl_put_mysql_rows", "zdl_rows_last_error",
@@ -152,6 +154,20 @@ def lib() -> C.CDLL:
     L.zdl_store_compact.restype = C.c_int
     L.zdl_store_size.argtypes = [vp]
     L.zdl_store_size.restype = u64
+    L.zdl_store_append_traced.argtypes = [vp, C.POINTER(SpanCols), vp, u64]
+    L.zdl_store_append_traced.restype = C.c_int
+    L.zdl_store_alive.argtypes = [vp]
+    L.zdl_store_alive.restype = u64
+    L.zdl_store_evict.argtypes = [vp, u64, C.POINTER(u64)]
+    L.zdl_store_evict.restype = C.c_int
+    L.zdl_store_compact_evicted.argtypes = [vp]
+    L.zdl_store_compact_evicted.restype = C.c_int
+    L.zdl_store_select.argtypes = [vp, C.c_int, C.POINTER(u64), C.POINTER(u64)]
+    L.zdl_store_select.restype = C.c_int
+    L.zdl_store_selection.argtypes = [vp, vp, vp]
+    L.zdl_store_selection.restype = C.c_int
+    L.zdl_put_selection.argtypes = [vp, vp]
+    L.zdl_put_selection.restype = C.c_int
     L.zdl_put_stored.argtypes = [vp, vp, vp, u64, vp, u64]
     L.zdl_put_stored.restype = C.c_int
     L.zdl_stream.restype = vp
@@ -366,6 +382,10 @@ class Context:
         off = np.ascontiguousarray(offsets, np.uint64)
         self.check(self._L.zdl_put_stored(self.h, store.h, _ptr(pm), len(pm), _ptr(off), len(off) - 1))
 
+    def put_selection(self, store: "Store") -> None:
+        """zdl_put_selection: link the store's current selection (Store.select), device-resident."""
+        self.check(self._L.zdl_put_selection(self.h, store.h))
+
     def merge_links(self, parent, child, call, err):
         p, c = np.ascontiguousarray(parent, np.int32), np.ascontiguousarray(child, np.int32)
         n, e = np.ascontiguousarray(call, np.int64), np.ascontiguousarray(err, np.int64)
@@ -407,18 +427,22 @@ class Store:
         self.h = C.c_void_p(h)
         self._L = L
 
-    def append_device(self, dev: SpanCols, n: int) -> None:
-        """Appends device columns (e.g. a Decoder's output) without a host round trip."""
-        rc = self._L.zdl_store_append(self.h, C.byref(dev), int(n))
+    def _check(self, rc: int) -> None:
         if rc != ZDL_OK:
             raise ZdlError(rc, self._L.zdl_store_last_error(self.h).decode())
 
-    def append(self, cols) -> None:
-        sc = SpanCols(None, _ptr(cols.id), _ptr(cols.parent_id), _ptr(cols.local_svc), _ptr(cols.remote_svc),
-                      _ptr(cols.local_ip4), _ptr(cols.local_ip6), _ptr(cols.port_flags), _ptr(cols.timestamp))
-        rc = self._L.zdl_store_append(self.h, C.byref(sc), cols.n_spans)
-        if rc != ZDL_OK:
-            raise ZdlError(rc, self._L.zdl_store_last_error(self.h).decode())
+    def append_device(self, dev: SpanCols, n: int) -> None:
+        """Appends device columns (e.g. a Decoder's output, trace_lo included) without a host
+        round trip; high trace ids 0."""
+        self._check(self._L.zdl_store_append(self.h, C.byref(dev), int(n)))
+
+    def append(self, cols, trace_hi: Optional[np.ndarray] = None) -> None:
+        """Appends host columns with their trace ids (trace_hi: high 64 bits, None = 0)."""
+        hi = None if trace_hi is None else np.ascontiguousarray(trace_hi, np.uint64)
+        sc = SpanCols(_ptr(cols.trace_lo), _ptr(cols.id), _ptr(cols.parent_id), _ptr(cols.local_svc),
+                      _ptr(cols.remote_svc), _ptr(cols.local_ip4), _ptr(cols.local_ip6), _ptr(cols.port_flags),
+                      _ptr(cols.timestamp))
+        self._check(self._L.zdl_store_append_traced(self.h, C.byref(sc), _ptr(hi), cols.n_spans))
 
     def clear(self) -> None:
         self._L.zdl_store_clear(self.h)
@@ -426,9 +450,36 @@ class Store:
     def compact(self, keep: np.ndarray) -> None:
         """zdl_store_compact: keep the spans at these ascending positions, renumbered 0..n."""
         k = np.ascontiguousarray(keep, np.uint32)
-        rc = self._L.zdl_store_compact(self.h, _ptr(k), len(k))
-        if rc != ZDL_OK:
-            raise ZdlError(rc, self._L.zdl_store_last_error(self.h).decode())
+        self._check(self._L.zdl_store_compact(self.h, _ptr(k), len(k)))
+
+    def compact_evicted(self) -> None:
+        """zdl_store_compact_evicted: free the evicted spans, renumbering the alive ones."""
+        self._check(self._L.zdl_store_compact_evicted(self.h))
+
+    def evict(self, to_recover: int) -> int:
+        """zdl_store_evict (evictToRecoverSpans): returns the number of spans evicted. Raises
+        ZdlError(ZDL_EREF_NSE) when the store runs empty first."""
+        ev = C.c_uint64(0)
+        self._check(self._L.zdl_store_evict(self.h, max(int(to_recover), 0), C.byref(ev)))
+        return int(ev.value)
+
+    @property
+    def alive(self) -> int:
+        return int(self._L.zdl_store_alive(self.h))
+
+    def select(self, mode: int):
+        """zdl_store_select: computes the selection on the device; returns (n_sel, n_traces)."""
+        n, t = C.c_uint64(0), C.c_uint64(0)
+        self._check(self._L.zdl_store_select(self.h, int(mode), C.byref(n), C.byref(t)))
+        return int(n.value), int(t.value)
+
+    def selection(self, mode: int):
+        """The selection copied out: (u32 positions, u64 CSR trace offsets)."""
+        n, t = self.select(mode)
+        perm = np.empty(n, np.uint32)
+        off = np.zeros(t + 1, np.uint64)
+        self._check(self._L.zdl_store_selection(self.h, _ptr(perm), _ptr(off)))
+        return perm, off
 
     def __len__(self) -> int:
         return int(self._L.zdl_store_size(self.h))

@@ -17,6 +17,7 @@
 #include <rccl/rccl.h>
 
 #include "zdl_group.h"
+#include "zdl_store_index.h"
 
 #include <hipcub/hipcub.hpp>
 
@@ -2097,17 +2098,24 @@ static int put_spans_ungrouped(zdl_ctx* c, const zdl_span_cols* col, uint64_t n)
 
 // ------------------------------------------------------------------ span store
 // A device-resident column store (the ingest side of InMemoryStorage):
-// accepted spans are appended to HBM columns once; a query uploads only the selection
-// (a u32 permutation in storage order + CSR offsets) and gathers on the device.
+// accepted spans are appended to HBM columns once, with their trace ids, timestamps and an
+// alive byte; eviction and a query's trace selection run on the device (zdl_store.hip) and the
+// selection is gathered and linked without leaving HBM.
 struct zdl_store {
   int device = 0;
   hipStream_t stream = nullptr;
   std::string err;
-  uint64_t n = 0, cap = 0;
-  DevBuf<uint64_t> id, pid;
+  uint64_t n = 0, cap = 0, n_alive = 0;
+  DevBuf<uint64_t> id, pid, lo, hi;
   DevBuf<int32_t> lsvc, rsvc, ip4, ip6;
   DevBuf<uint32_t> pf;
   DevBuf<int64_t> ts;
+  DevBuf<uint8_t> alive;
+  zdl::IndexWork iw;
+  DevBuf<uint32_t> sel;  // the last zdl_store_select: positions in trace order
+  DevBuf<uint64_t> sel_off;  // and its CSR trace offsets
+  uint64_t sel_n = 0, sel_traces = 0;
+  bool sel_valid = false;
 };
 
 }  // extern "C"
@@ -2130,6 +2138,103 @@ int store_fail(zdl_store* st, int code, const std::string& msg) {
   if (st) st->err = msg;
   return code;
 }
+int store_hip_fail(zdl_store* st, hipError_t e, const char* where) {
+  return store_fail(st, e == hipErrorOutOfMemory ? ZDL_ENOMEM : ZDL_EDEVICE,
+                    std::string(where) + ": " + hipGetErrorString(e));
+}
+
+__global__ void k_gather_index(const uint64_t* __restrict__ lo, const uint64_t* __restrict__ hi,
+                               const uint8_t* __restrict__ alive, const uint32_t* __restrict__ idx, uint64_t n,
+                               uint64_t* __restrict__ lo_o, uint64_t* __restrict__ hi_o, uint8_t* __restrict__ alive_o) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t j = idx[i];
+  lo_o[i] = lo[j];
+  hi_o[i] = hi[j];
+  alive_o[i] = alive[j];
+}
+
+// Keeps the stored spans idx[0..n_keep) (device, ascending) and frees the rest.
+hipError_t store_compact_dev(zdl_store* st, const uint32_t* idx, uint64_t n_keep) {
+  const hipStream_t s = st->stream;
+  const uint64_t cap = std::max<uint64_t>(2 * n_keep, 1 << 16);
+  DevBuf<uint64_t> id, pid, lo, hi;
+  DevBuf<int32_t> lsvc, rsvc, ip4, ip6;
+  DevBuf<uint32_t> pf;
+  DevBuf<int64_t> ts;
+  DevBuf<uint8_t> alive;
+  hipError_t e = id.ensure(cap);
+  if (e == hipSuccess) e = pid.ensure(cap);
+  if (e == hipSuccess) e = lo.ensure(cap);
+  if (e == hipSuccess) e = hi.ensure(cap);
+  if (e == hipSuccess) e = lsvc.ensure(cap);
+  if (e == hipSuccess) e = rsvc.ensure(cap);
+  if (e == hipSuccess) e = ip4.ensure(cap);
+  if (e == hipSuccess) e = ip6.ensure(cap);
+  if (e == hipSuccess) e = pf.ensure(cap);
+  if (e == hipSuccess) e = ts.ensure(cap);
+  if (e == hipSuccess) e = alive.ensure(cap);
+  if (e == hipSuccess && n_keep) {
+    const Cols in{st->id.p, st->pid.p, st->lsvc.p, st->rsvc.p, st->ip4.p, st->ip6.p, st->pf.p, st->ts.p};
+    const dim3 g((unsigned)((n_keep + 255) / 256));
+    hipLaunchKernelGGL(k_gather, g, dim3(256), 0, s, in, idx, n_keep, id.p, pid.p, lsvc.p, rsvc.p, ip4.p, ip6.p,
+                       pf.p, ts.p);
+    e = hipGetLastError();
+    if (e == hipSuccess) {
+      hipLaunchKernelGGL(k_gather_index, g, dim3(256), 0, s, st->lo.p, st->hi.p, st->alive.p, idx, n_keep, lo.p,
+                         hi.p, alive.p);
+      e = hipGetLastError();
+    }
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    id.release(); pid.release(); lo.release(); hi.release(); lsvc.release(); rsvc.release(); ip4.release();
+    ip6.release(); pf.release(); ts.release(); alive.release();
+    return e;
+  }
+  st->id.release(); st->pid.release(); st->lo.release(); st->hi.release(); st->lsvc.release(); st->rsvc.release();
+  st->ip4.release(); st->ip6.release(); st->pf.release(); st->ts.release(); st->alive.release();
+  st->id = id; st->pid = pid; st->lo = lo; st->hi = hi; st->lsvc = lsvc; st->rsvc = rsvc; st->ip4 = ip4;
+  st->ip6 = ip6; st->pf = pf; st->ts = ts; st->alive = alive;
+  st->n = n_keep;
+  st->cap = cap;
+  st->sel_valid = false;
+  return hipSuccess;
+}
+
+// Gathers the selection perm[0..n_sel) (device) of the store and links it as the CSR traces
+// off[0..n_traces] (device), like zdl_put_spans on the gathered columns.
+int put_stored_dev(zdl_ctx* c, const zdl_store* st, const uint32_t* perm, uint64_t n_sel, const uint64_t* off,
+                   uint64_t n_traces) {
+  const hipStream_t s = c->stream;
+  HIP_TRY(c, c->g_id.ensure(n_sel));
+  HIP_TRY(c, c->g_pid.ensure(n_sel));
+  HIP_TRY(c, c->g_lsvc.ensure(n_sel));
+  HIP_TRY(c, c->g_rsvc.ensure(n_sel));
+  HIP_TRY(c, c->g_ip4.ensure(n_sel));
+  HIP_TRY(c, c->g_ip6.ensure(n_sel));
+  HIP_TRY(c, c->g_pf.ensure(n_sel));
+  const bool with_ts = c->window || c->days;
+  if (with_ts) HIP_TRY(c, c->g_ts.ensure(n_sel));
+  const Cols in{st->id.p, st->pid.p, st->lsvc.p, st->rsvc.p, st->ip4.p, st->ip6.p, st->pf.p,
+                with_ts ? st->ts.p : nullptr};
+  hipLaunchKernelGGL(k_gather, dim3((unsigned)((n_sel + 255) / 256)), dim3(256), 0, s, in, perm, n_sel,
+                     c->g_id.p, c->g_pid.p, c->g_lsvc.p, c->g_rsvc.p, c->g_ip4.p, c->g_ip6.p, c->g_pf.p,
+                     with_ts ? c->g_ts.p : nullptr);
+  HIP_TRY(c, hipGetLastError());
+  zdl_span_cols g{};
+  g.id = c->g_id.p;
+  g.parent_id = c->g_pid.p;
+  g.local_svc = c->g_lsvc.p;
+  g.remote_svc = c->g_rsvc.p;
+  g.local_ip4 = c->g_ip4.p;
+  g.local_ip6 = c->g_ip6.p;
+  g.port_flags = c->g_pf.p;
+  g.timestamp = with_ts ? c->g_ts.p : nullptr;
+  const int rc = put_spans_link(c, &g, n_sel, off, n_traces);
+  if (rc != ZDL_OK) return rc;
+  return zdl_sync(c);
+}
 }  // namespace
 extern "C" {
 
@@ -2148,8 +2253,10 @@ void zdl_store_destroy(zdl_store* st) {
   if (!st) return;
   (void)hipSetDevice(st->device);
   (void)hipStreamSynchronize(st->stream);
-  st->id.release(); st->pid.release(); st->lsvc.release(); st->rsvc.release(); st->ip4.release();
-  st->ip6.release(); st->pf.release(); st->ts.release();
+  st->id.release(); st->pid.release(); st->lo.release(); st->hi.release(); st->lsvc.release(); st->rsvc.release();
+  st->ip4.release(); st->ip6.release(); st->pf.release(); st->ts.release(); st->alive.release();
+  st->sel.release(); st->sel_off.release();
+  st->iw.release();
   (void)hipStreamDestroy(st->stream);
   delete st;
 }
@@ -2158,19 +2265,22 @@ const char* zdl_store_last_error(const zdl_store* st) { return st ? st->err.c_st
 
 uint64_t zdl_store_size(const zdl_store* st) { return st ? st->n : 0; }
 
+uint64_t zdl_store_alive(const zdl_store* st) { return st ? st->n_alive : 0; }
+
 int zdl_store_clear(zdl_store* st) {
   if (!st) return ZDL_EINVAL;
-  st->n = 0;
+  st->n = st->n_alive = 0;
+  st->sel_valid = false;
   return ZDL_OK;
 }
 
-int zdl_store_append(zdl_store* st, const zdl_span_cols* col, uint64_t n) {
+int zdl_store_append_traced(zdl_store* st, const zdl_span_cols* col, const uint64_t* trace_hi, uint64_t n) {
   if (!st || !col) return ZDL_EINVAL;
   if (n == 0) return ZDL_OK;
   if (!col->id || !col->parent_id || !col->local_svc || !col->remote_svc || !col->local_ip4 || !col->local_ip6 ||
       !col->port_flags)
     return store_fail(st, ZDL_EINVAL, "zdl_store_append: missing column");
-  if (st->n + n >= (1ull << 32)) return store_fail(st, ZDL_EINVAL, "zdl_store_append: store limited to 2^32 spans");
+  if (st->n + n >= (1ull << 31)) return store_fail(st, ZDL_EINVAL, "zdl_store_append: store limited to 2^31 spans");
   (void)hipGetLastError();
   hipError_t e = hipSetDevice(st->device);
   const hipStream_t s = st->stream;
@@ -2178,17 +2288,26 @@ int zdl_store_append(zdl_store* st, const zdl_span_cols* col, uint64_t n) {
     const uint64_t cap = std::max<uint64_t>(st->n + n, std::max<uint64_t>(2 * st->cap, 1 << 16));
     if (e == hipSuccess) e = store_grow(st->id, st->n, cap, s);
     if (e == hipSuccess) e = store_grow(st->pid, st->n, cap, s);
+    if (e == hipSuccess) e = store_grow(st->lo, st->n, cap, s);
+    if (e == hipSuccess) e = store_grow(st->hi, st->n, cap, s);
     if (e == hipSuccess) e = store_grow(st->lsvc, st->n, cap, s);
     if (e == hipSuccess) e = store_grow(st->rsvc, st->n, cap, s);
     if (e == hipSuccess) e = store_grow(st->ip4, st->n, cap, s);
     if (e == hipSuccess) e = store_grow(st->ip6, st->n, cap, s);
     if (e == hipSuccess) e = store_grow(st->pf, st->n, cap, s);
     if (e == hipSuccess) e = store_grow(st->ts, st->n, cap, s);
+    if (e == hipSuccess) e = store_grow(st->alive, st->n, cap, s);
     if (e == hipSuccess) st->cap = cap;
   }
   const uint64_t o = st->n;
   if (e == hipSuccess) e = hipMemcpyAsync(st->id.p + o, col->id, n * 8, hipMemcpyDefault, s);
   if (e == hipSuccess) e = hipMemcpyAsync(st->pid.p + o, col->parent_id, n * 8, hipMemcpyDefault, s);
+  if (e == hipSuccess)
+    e = col->trace_lo ? hipMemcpyAsync(st->lo.p + o, col->trace_lo, n * 8, hipMemcpyDefault, s)
+                      : hipMemsetAsync(st->lo.p + o, 0, n * 8, s);
+  if (e == hipSuccess)
+    e = trace_hi ? hipMemcpyAsync(st->hi.p + o, trace_hi, n * 8, hipMemcpyDefault, s)
+                 : hipMemsetAsync(st->hi.p + o, 0, n * 8, s);
   if (e == hipSuccess) e = hipMemcpyAsync(st->lsvc.p + o, col->local_svc, n * 4, hipMemcpyDefault, s);
   if (e == hipSuccess) e = hipMemcpyAsync(st->rsvc.p + o, col->remote_svc, n * 4, hipMemcpyDefault, s);
   if (e == hipSuccess) e = hipMemcpyAsync(st->ip4.p + o, col->local_ip4, n * 4, hipMemcpyDefault, s);
@@ -2197,12 +2316,17 @@ int zdl_store_append(zdl_store* st, const zdl_span_cols* col, uint64_t n) {
   if (e == hipSuccess)
     e = col->timestamp ? hipMemcpyAsync(st->ts.p + o, col->timestamp, n * 8, hipMemcpyDefault, s)
                        : hipMemsetAsync(st->ts.p + o, 0, n * 8, s);
+  if (e == hipSuccess) e = hipMemsetAsync(st->alive.p + o, 1, n, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);  // the columns are borrowed for the call only
-  if (e != hipSuccess)
-    return store_fail(st, e == hipErrorOutOfMemory ? ZDL_ENOMEM : ZDL_EDEVICE,
-                      std::string("zdl_store_append: ") + hipGetErrorString(e));
+  if (e != hipSuccess) return store_hip_fail(st, e, "zdl_store_append");
   st->n += n;
+  st->n_alive += n;
+  st->sel_valid = false;
   return ZDL_OK;
+}
+
+int zdl_store_append(zdl_store* st, const zdl_span_cols* col, uint64_t n) {
+  return zdl_store_append_traced(st, col, nullptr, n);
 }
 
 int zdl_store_compact(zdl_store* st, const uint32_t* keep, uint64_t n_keep) {
@@ -2213,42 +2337,97 @@ int zdl_store_compact(zdl_store* st, const uint32_t* keep, uint64_t n_keep) {
       return store_fail(st, ZDL_EINVAL, "zdl_store_compact: positions must ascend inside the store");
   (void)hipGetLastError();
   hipError_t e = hipSetDevice(st->device);
-  const hipStream_t s = st->stream;
-  const uint64_t cap = std::max<uint64_t>(2 * n_keep, 1 << 16);
-  DevBuf<uint64_t> id, pid;
-  DevBuf<int32_t> lsvc, rsvc, ip4, ip6;
-  DevBuf<uint32_t> pf, idx;
-  DevBuf<int64_t> ts;
-  if (e == hipSuccess) e = id.ensure(cap);
-  if (e == hipSuccess) e = pid.ensure(cap);
-  if (e == hipSuccess) e = lsvc.ensure(cap);
-  if (e == hipSuccess) e = rsvc.ensure(cap);
-  if (e == hipSuccess) e = ip4.ensure(cap);
-  if (e == hipSuccess) e = ip6.ensure(cap);
-  if (e == hipSuccess) e = pf.ensure(cap);
-  if (e == hipSuccess) e = ts.ensure(cap);
+  DevBuf<uint32_t> idx;
   if (e == hipSuccess) e = idx.ensure(std::max<uint64_t>(n_keep, 1));
-  if (e == hipSuccess && n_keep) e = hipMemcpyAsync(idx.p, keep, n_keep * 4, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess && n_keep) {
-    const Cols in{st->id.p, st->pid.p, st->lsvc.p, st->rsvc.p, st->ip4.p, st->ip6.p, st->pf.p, st->ts.p};
-    hipLaunchKernelGGL(k_gather, dim3((unsigned)((n_keep + 255) / 256)), dim3(256), 0, s, in, idx.p, n_keep, id.p,
-                       pid.p, lsvc.p, rsvc.p, ip4.p, ip6.p, pf.p, ts.p);
-    e = hipGetLastError();
-  }
-  if (e == hipSuccess) e = hipStreamSynchronize(s);
-  if (e != hipSuccess) {
-    id.release(); pid.release(); lsvc.release(); rsvc.release(); ip4.release(); ip6.release(); pf.release();
-    ts.release(); idx.release();
-    return store_fail(st, e == hipErrorOutOfMemory ? ZDL_ENOMEM : ZDL_EDEVICE,
-                      std::string("zdl_store_compact: ") + hipGetErrorString(e));
-  }
-  st->id.release(); st->pid.release(); st->lsvc.release(); st->rsvc.release(); st->ip4.release();
-  st->ip6.release(); st->pf.release(); st->ts.release();
-  st->id = id; st->pid = pid; st->lsvc = lsvc; st->rsvc = rsvc; st->ip4 = ip4; st->ip6 = ip6; st->pf = pf; st->ts = ts;
+  if (e == hipSuccess && n_keep) e = hipMemcpyAsync(idx.p, keep, n_keep * 4, hipMemcpyHostToDevice, st->stream);
+  if (e == hipSuccess) e = store_compact_dev(st, idx.p, n_keep);
+  uint64_t alive = 0;
+  if (e == hipSuccess) e = zdl::index_alive(st->iw, st->alive.p, st->n, idx.p, &alive, st->stream);
   idx.release();
-  st->n = n_keep;
-  st->cap = cap;
+  if (e != hipSuccess) return store_hip_fail(st, e, "zdl_store_compact");
+  st->n_alive = alive;
   return ZDL_OK;
+}
+
+int zdl_store_compact_evicted(zdl_store* st) {
+  if (!st) return ZDL_EINVAL;
+  if (st->n_alive == st->n) return ZDL_OK;
+  (void)hipGetLastError();
+  hipError_t e = hipSetDevice(st->device);
+  DevBuf<uint32_t> idx;
+  uint64_t m = 0;
+  if (e == hipSuccess) e = idx.ensure(std::max<uint64_t>(st->n, 1));
+  if (e == hipSuccess) e = zdl::index_alive(st->iw, st->alive.p, st->n, idx.p, &m, st->stream);
+  if (e == hipSuccess) e = store_compact_dev(st, idx.p, m);
+  idx.release();
+  if (e != hipSuccess) return store_hip_fail(st, e, "zdl_store_compact_evicted");
+  st->n_alive = m;
+  return ZDL_OK;
+}
+
+int zdl_store_evict(zdl_store* st, uint64_t to_recover, uint64_t* evicted) {
+  if (!st) return ZDL_EINVAL;
+  if (evicted) *evicted = 0;
+  if (to_recover == 0) return ZDL_OK;
+  (void)hipGetLastError();
+  hipError_t e = hipSetDevice(st->device);
+  uint64_t ev = 0;
+  bool exhausted = false;
+  if (e == hipSuccess)
+    e = zdl::index_evict(st->iw, st->lo.p, st->ts.p, st->alive.p, st->n, to_recover, &ev, &exhausted, st->stream);
+  if (e != hipSuccess) return store_hip_fail(st, e, "zdl_store_evict");
+  st->n_alive -= ev;
+  st->sel_valid = false;
+  if (evicted) *evicted = ev;
+  if (exhausted)
+    return store_fail(st, ZDL_EREF_NSE, "zdl_store_evict: the store ran empty (TreeMap.lastKey of an empty map)");
+  return ZDL_OK;
+}
+
+int zdl_store_select(zdl_store* st, int mode, uint64_t* n_sel, uint64_t* n_traces) {
+  if (!st) return ZDL_EINVAL;
+  if (mode != ZDL_SELECT_NEWEST && mode != ZDL_SELECT_ALL && mode != ZDL_SELECT_ALL_STRICT)
+    return store_fail(st, ZDL_EINVAL, "zdl_store_select: unknown mode");
+  (void)hipGetLastError();
+  st->sel_valid = false;
+  hipError_t e = hipSetDevice(st->device);
+  if (e == hipSuccess) e = st->sel.ensure(std::max<uint64_t>(st->n, 1));
+  if (e == hipSuccess) e = st->sel_off.ensure(st->n + 1);
+  const int m = mode == ZDL_SELECT_NEWEST ? zdl::SEL_NEWEST : mode == ZDL_SELECT_ALL ? zdl::SEL_ALL : zdl::SEL_ALL_STRICT;
+  if (e == hipSuccess)
+    e = zdl::index_select(st->iw, st->lo.p, st->hi.p, st->ts.p, st->alive.p, st->n, m, st->sel.p, st->sel_off.p,
+                          &st->sel_n, &st->sel_traces, st->stream);
+  if (e != hipSuccess) return store_hip_fail(st, e, "zdl_store_select");
+  st->sel_valid = true;
+  if (n_sel) *n_sel = st->sel_n;
+  if (n_traces) *n_traces = st->sel_traces;
+  return ZDL_OK;
+}
+
+int zdl_store_selection(const zdl_store* cst, uint32_t* perm, uint64_t* trace_offsets) {
+  zdl_store* st = const_cast<zdl_store*>(cst);
+  if (!st) return ZDL_EINVAL;
+  if (!st->sel_valid) return store_fail(st, ZDL_EINVAL, "zdl_store_selection: no current selection");
+  hipError_t e = hipSetDevice(st->device);
+  if (e == hipSuccess && perm && st->sel_n)
+    e = hipMemcpyAsync(perm, st->sel.p, st->sel_n * 4, hipMemcpyDeviceToHost, st->stream);
+  if (e == hipSuccess && trace_offsets && st->sel_traces)
+    e = hipMemcpyAsync(trace_offsets, st->sel_off.p, (st->sel_traces + 1) * 8, hipMemcpyDeviceToHost, st->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(st->stream);
+  if (e != hipSuccess) return store_hip_fail(st, e, "zdl_store_selection");
+  if (trace_offsets && !st->sel_traces) trace_offsets[0] = 0;
+  return ZDL_OK;
+}
+
+int zdl_put_selection(zdl_ctx* c, const zdl_store* st) {
+  if (!c || !st) return fail(c, ZDL_EINVAL, "null argument");
+  if (!c->sub.empty()) return fail(c, ZDL_EINVAL, "zdl_put_selection: a store lives on one device");
+  if (st->device != c->device) return fail(c, ZDL_EINVAL, "zdl_put_selection: store and context on different devices");
+  if (!st->sel_valid) return fail(c, ZDL_EINVAL, "zdl_put_selection: no current selection (zdl_store_select)");
+  if (st->sel_traces == 0) return ZDL_OK;
+  HIP_TRY(c, enter(c));
+  HIP_TRY(c, hipStreamSynchronize(st->stream));
+  return put_stored_dev(c, st, st->sel.p, st->sel_n, st->sel_off.p, st->sel_traces);
 }
 
 int zdl_put_stored(zdl_ctx* c, const zdl_store* st, const uint32_t* perm, uint64_t n_sel, const uint64_t* off,
@@ -2264,38 +2443,11 @@ int zdl_put_stored(zdl_ctx* c, const zdl_store* st, const uint32_t* perm, uint64
     if (perm[i] >= st->n) return fail(c, ZDL_EINVAL, "zdl_put_stored: selection outside the store");
   HIP_TRY(c, enter(c));
   HIP_TRY(c, hipStreamSynchronize(st->stream));
-  const hipStream_t s = c->stream;
   HIP_TRY(c, c->h_ord.ensure(n_sel));
   HIP_TRY(c, c->h_off.ensure(n_traces + 1));
-  HIP_TRY(c, hipMemcpyAsync(c->h_ord.p, perm, n_sel * 4, hipMemcpyHostToDevice, s));
-  HIP_TRY(c, hipMemcpyAsync(c->h_off.p, off, (n_traces + 1) * 8, hipMemcpyHostToDevice, s));
-  HIP_TRY(c, c->g_id.ensure(n_sel));
-  HIP_TRY(c, c->g_pid.ensure(n_sel));
-  HIP_TRY(c, c->g_lsvc.ensure(n_sel));
-  HIP_TRY(c, c->g_rsvc.ensure(n_sel));
-  HIP_TRY(c, c->g_ip4.ensure(n_sel));
-  HIP_TRY(c, c->g_ip6.ensure(n_sel));
-  HIP_TRY(c, c->g_pf.ensure(n_sel));
-  const bool with_ts = c->window || c->days;
-  if (with_ts) HIP_TRY(c, c->g_ts.ensure(n_sel));
-  const Cols in{st->id.p, st->pid.p, st->lsvc.p, st->rsvc.p, st->ip4.p, st->ip6.p, st->pf.p,
-                with_ts ? st->ts.p : nullptr};
-  hipLaunchKernelGGL(k_gather, dim3((unsigned)((n_sel + 255) / 256)), dim3(256), 0, s, in, c->h_ord.p, n_sel,
-                     c->g_id.p, c->g_pid.p, c->g_lsvc.p, c->g_rsvc.p, c->g_ip4.p, c->g_ip6.p, c->g_pf.p,
-                     with_ts ? c->g_ts.p : nullptr);
-  HIP_TRY(c, hipGetLastError());
-  zdl_span_cols g{};
-  g.id = c->g_id.p;
-  g.parent_id = c->g_pid.p;
-  g.local_svc = c->g_lsvc.p;
-  g.remote_svc = c->g_rsvc.p;
-  g.local_ip4 = c->g_ip4.p;
-  g.local_ip6 = c->g_ip6.p;
-  g.port_flags = c->g_pf.p;
-  g.timestamp = with_ts ? c->g_ts.p : nullptr;
-  const int rc = put_spans_link(c, &g, n_sel, c->h_off.p, n_traces);
-  if (rc != ZDL_OK) return rc;
-  return zdl_sync(c);
+  HIP_TRY(c, hipMemcpyAsync(c->h_ord.p, perm, n_sel * 4, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(c->h_off.p, off, (n_traces + 1) * 8, hipMemcpyHostToDevice, c->stream));
+  return put_stored_dev(c, st, c->h_ord.p, n_sel, c->h_off.p, n_traces);
 }
 
 int zdl_put_spans_device(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans, const uint64_t* off,

@@ -1,0 +1,431 @@
+// zdl_store.hip — InMemoryStorage's trace index on the device (zdl_store_index.h).
+//
+// All passes are HBM-bound gathers, flag/scan kernels and stable LSD radix sorts (hipCUB) over
+// the alive spans: a getDependencies selection is four 64-bit (key, u32 position) sorts plus a
+// sort of one key per trace, an eviction one span sort and one trace sort. Counts (alive spans,
+// traces, the eviction result) are the only values that come back to the host.
+#include "zdl_store_index.h"
+
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+
+namespace zdl {
+namespace {
+
+constexpr uint64_t kSign = 1ull << 63;  // int64 -> order-preserving uint64
+
+inline dim3 grid_of(uint64_t n) { return dim3((unsigned)std::max<uint64_t>((n + 255) / 256, 1)); }
+
+#define ITRY(expr)                   \
+  do {                               \
+    hipError_t _e = (expr);          \
+    if (_e != hipSuccess) return _e; \
+  } while (0)
+
+// ZDL_INDEX_TRACE=1: synchronise after every step and name the one that fails (diagnostics)
+bool trace_steps() {
+  static const bool on = getenv("ZDL_INDEX_TRACE") != nullptr;
+  return on;
+}
+hipError_t step_done(hipStream_t s, int line) {
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess && trace_steps()) e = hipStreamSynchronize(s);
+  if (e != hipSuccess && trace_steps()) fprintf(stderr, "zdl_store.hip:%d: %s\n", line, hipGetErrorString(e));
+  return e;
+}
+
+#define LAUNCH(kernel, n, ...)                                                    \
+  do {                                                                            \
+    hipLaunchKernelGGL(kernel, grid_of(n), dim3(256), 0, s, __VA_ARGS__);          \
+    ITRY(step_done(s, __LINE__));                                                 \
+  } while (0)
+
+// key[i] = src[idx[i]] ^ x  (x = kSign turns a timestamp into an unsigned key)
+__global__ void k_take(const uint64_t* __restrict__ src, const uint32_t* __restrict__ idx, uint64_t x,
+                       uint64_t* __restrict__ key, uint64_t m) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < m) key[i] = src[idx[i]] ^ x;
+}
+
+// key[i] = src[outer[inner[i]]]
+__global__ void k_take2(const uint64_t* __restrict__ src, const uint32_t* __restrict__ outer,
+                        const uint32_t* __restrict__ inner, uint64_t* __restrict__ key, uint64_t m) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < m) key[i] = src[outer[inner[i]]];
+}
+
+__global__ void k_iota32(uint32_t* __restrict__ out, uint64_t m) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < m) out[i] = (uint32_t)i;
+}
+
+// flag[i] = a new run of equal keys starts at i (keys sorted)
+__global__ void k_runs(const uint64_t* __restrict__ key, uint64_t m, uint8_t* __restrict__ flag) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < m) flag[i] = i == 0 || key[i] != key[i - 1];
+}
+
+// flag[i] = a trace starts at position i of perm (low id changes; or high id, when given)
+__global__ void k_trace_heads(const uint64_t* __restrict__ lo, const uint64_t* __restrict__ hi,
+                              const uint32_t* __restrict__ perm, uint64_t m, uint8_t* __restrict__ flag) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  bool h = i == 0;
+  if (!h) {
+    const uint32_t a = perm[i - 1], b = perm[i];
+    h = lo[a] != lo[b] || (hi && hi[a] != hi[b]);
+  }
+  flag[i] = h;
+}
+
+__global__ void k_close(uint64_t* __restrict__ off, const uint64_t* __restrict__ count, uint64_t m) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) off[*count] = m;
+}
+
+__global__ void k_widen(const uint8_t* __restrict__ flag, uint64_t m, uint32_t* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < m) out[i] = flag[i];
+}
+
+// (lowTraceId, timestamp) key runs over v (sorted by low id, timestamp, position):
+// out[i] = i where a key starts, else 0 (a max-scan then names each span's key head)
+__global__ void k_key_heads(const uint64_t* __restrict__ lo, const int64_t* __restrict__ ts,
+                            const uint32_t* __restrict__ v, uint64_t m, uint32_t* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  bool h = i == 0;
+  if (!h) {
+    const uint32_t a = v[i - 1], b = v[i];
+    h = lo[a] != lo[b] || ts[a] != ts[b];
+  }
+  out[i] = h ? (uint32_t)i : 0u;
+}
+
+// storage-order key: (first arrival of the span's (lowTraceId, timestamp) key, arrival)
+__global__ void k_first_seen(const uint32_t* __restrict__ v, const uint32_t* __restrict__ head,
+                             uint64_t m, uint64_t* __restrict__ key) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < m) key[i] = ((uint64_t)v[head[i]] << 32) | v[i];
+}
+
+// segment j's newest timestamp (the last span of j in v, sorted by timestamp inside a low id),
+// as a descending key; segments fed in reverse (descending low id) so a stable sort breaks
+// newest-timestamp ties by descending low id
+__global__ void k_seg_newest(const uint64_t* __restrict__ seg, uint64_t T, const uint32_t* __restrict__ v,
+                             const int64_t* __restrict__ ts, uint64_t* __restrict__ key, uint32_t* __restrict__ val) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= T) return;
+  const uint64_t newest = (uint64_t)ts[v[seg[j + 1] - 1]] ^ kSign;
+  key[T - 1 - j] = ~newest;
+  val[T - 1 - j] = (uint32_t)j;
+}
+
+// segment j's smallest timestamp (eviction order key); segments come in ascending low id
+__global__ void k_seg_oldest(const uint64_t* __restrict__ seg, uint64_t T, const uint32_t* __restrict__ v,
+                             const int64_t* __restrict__ ts, uint64_t* __restrict__ key, uint32_t* __restrict__ val) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= T) return;
+  uint64_t best = ~0ull;
+  for (uint64_t e = seg[j]; e < seg[j + 1]; ++e) best = std::min(best, (uint64_t)ts[v[e]] ^ kSign);
+  key[j] = best;
+  val[j] = (uint32_t)j;
+}
+
+__global__ void k_seg_sizes(const uint64_t* __restrict__ seg, const uint32_t* __restrict__ order, uint64_t T,
+                            uint32_t* __restrict__ size) {
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < T) size[r] = (uint32_t)(seg[order[r] + 1] - seg[order[r]]);
+}
+
+__global__ void k_rank_of(const uint32_t* __restrict__ order, uint64_t T, uint32_t* __restrict__ rank) {
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < T) rank[order[r]] = (uint32_t)r;
+}
+
+// moves span i of segment j (segid1 = j + 1) to its segment's new place
+__global__ void k_place(const uint32_t* __restrict__ v, const uint32_t* __restrict__ segid1,
+                        const uint64_t* __restrict__ seg, const uint32_t* __restrict__ rank,
+                        const uint32_t* __restrict__ start, uint64_t m, uint32_t* __restrict__ perm) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  const uint32_t j = segid1[i] - 1;
+  perm[start[rank[j]] + (i - seg[j])] = v[i];
+}
+
+__global__ void k_new_off(const uint32_t* __restrict__ start, uint64_t T, uint64_t m, uint64_t* __restrict__ off) {
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < T) off[r] = start[r];
+  if (r == T) off[T] = m;
+}
+
+// (lowTraceId, traceId) group heads over u (span indexes into v, grouped, ascending inside)
+__global__ void k_group_heads(const uint64_t* __restrict__ lo, const uint64_t* __restrict__ hi,
+                              const uint32_t* __restrict__ v, const uint32_t* __restrict__ u, uint64_t m,
+                              uint32_t* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  bool h = i == 0;
+  if (!h) {
+    const uint32_t a = v[u[i - 1]], b = v[u[i]];
+    h = lo[a] != lo[b] || hi[a] != hi[b];
+  }
+  out[i] = h ? (uint32_t)i : 0u;
+}
+
+__global__ void k_group_first(const uint32_t* __restrict__ u, const uint32_t* __restrict__ head, uint64_t m,
+                              uint32_t* __restrict__ first) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < m) first[u[i]] = u[head[i]];
+}
+
+__global__ void k_evict_init(uint64_t T, uint64_t m, uint64_t* __restrict__ d) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    d[1] = T - 1;  // not found: every trace goes (the store runs empty)
+    d[2] = m;
+    d[3] = 1;
+  }
+}
+
+// the first rank whose cumulative span count reaches R
+__global__ void k_evict_find(const uint32_t* __restrict__ cum, uint64_t T, uint64_t R, uint64_t* __restrict__ d) {
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= T) return;
+  const uint64_t c = cum[r], p = r ? cum[r - 1] : 0;
+  if (c >= R && p < R) {
+    d[1] = r;
+    d[2] = c;
+    d[3] = 0;
+  }
+}
+
+__global__ void k_evict_mark(const uint32_t* __restrict__ v, const uint32_t* __restrict__ segid1,
+                             const uint32_t* __restrict__ rank, const uint64_t* __restrict__ d, uint64_t m,
+                             uint8_t* __restrict__ alive) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < m && rank[segid1[i] - 1] <= d[1]) alive[v[i]] = 0;
+}
+
+template <class T>
+hipError_t grow(T*& p, size_t n) {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  return hipMalloc((void**)&p, std::max<size_t>(n, 1) * sizeof(T));
+}
+
+hipError_t reserve(IndexWork& w, uint64_t n) {
+  if (!w.d) {
+    ITRY(hipMalloc((void**)&w.d, 4 * sizeof(uint64_t)));
+    ITRY(hipHostMalloc((void**)&w.h, 4 * sizeof(uint64_t), hipHostMallocDefault));
+  }
+  if (n <= w.cap) return hipSuccess;
+  for (auto*& p : w.k) ITRY(grow(p, n));
+  for (auto*& p : w.v) ITRY(grow(p, n));
+  for (auto*& p : w.u) ITRY(grow(p, n));
+  for (auto*& p : w.sk) ITRY(grow(p, n));
+  for (auto*& p : w.sv) ITRY(grow(p, n));
+  ITRY(grow(w.seg, n + 1));
+  ITRY(grow(w.flag, n));
+  w.cap = n;
+  return hipSuccess;
+}
+
+// runs a hipCUB call twice: size query, then with (grown) scratch
+template <class F>
+hipError_t cub_at(IndexWork& w, hipStream_t s, int line, F f) {
+  size_t need = 0;
+  ITRY(f(nullptr, need));
+  if (need > w.tmp_bytes) {
+    if (w.tmp) (void)hipFree(w.tmp);
+    w.tmp = nullptr;
+    w.tmp_bytes = 0;
+    ITRY(hipMalloc(&w.tmp, need));
+    w.tmp_bytes = need;
+  }
+  size_t b = w.tmp_bytes;
+  ITRY(f(w.tmp, b));
+  return step_done(s, line);
+}
+
+hipError_t fetch(IndexWork& w, int k, hipStream_t s) {
+  ITRY(hipMemcpyAsync(w.h, w.d, k * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  return hipStreamSynchronize(s);
+}
+
+hipError_t sort64(IndexWork& w, const uint64_t* kin, uint64_t* kout, const uint32_t* vin, uint32_t* vout,
+                  uint64_t m, hipStream_t s) {
+  return cub_at(w, s, __LINE__, [&](void* t, size_t& b) {
+    return hipcub::DeviceRadixSort::SortPairs(t, b, kin, kout, vin, vout, (int)m, 0, 64, s);
+  });
+}
+
+hipError_t sort32(IndexWork& w, const uint32_t* kin, uint32_t* kout, const uint32_t* vin, uint32_t* vout,
+                  uint64_t m, hipStream_t s) {
+  return cub_at(w, s, __LINE__, [&](void* t, size_t& b) {
+    return hipcub::DeviceRadixSort::SortPairs(t, b, kin, kout, vin, vout, (int)m, 0, 32, s);
+  });
+}
+
+hipError_t max_scan(IndexWork& w, const uint32_t* in, uint32_t* out, uint64_t m, hipStream_t s) {
+  return cub_at(w, s, __LINE__, [&](void* t, size_t& b) {
+    return hipcub::DeviceScan::InclusiveScan(t, b, in, out, hipcub::Max(), (int)m, s);
+  });
+}
+
+hipError_t sum_scan(IndexWork& w, const uint32_t* in, uint32_t* out, uint64_t m, bool inclusive, hipStream_t s) {
+  return cub_at(w, s, __LINE__, [&](void* t, size_t& b) {
+    return inclusive ? hipcub::DeviceScan::InclusiveSum(t, b, in, out, (int)m, s)
+                     : hipcub::DeviceScan::ExclusiveSum(t, b, in, out, (int)m, s);
+  });
+}
+
+// the run heads of flag[0..m) as CSR offsets (off[0..T], T into w.d[0]); returns T
+hipError_t offsets_of(IndexWork& w, const uint8_t* flag, uint64_t m, uint64_t* off, uint64_t* T, hipStream_t s) {
+  ITRY(cub_at(w, s, __LINE__, [&](void* t, size_t& b) {
+    return hipcub::DeviceSelect::Flagged(t, b, hipcub::CountingInputIterator<uint64_t>(0), flag, off, w.d, (int)m, s);
+  }));
+  hipLaunchKernelGGL(k_close, dim3(1), dim3(64), 0, s, off, w.d, m);
+  ITRY(hipGetLastError());
+  ITRY(fetch(w, 1, s));
+  *T = w.h[0];
+  return hipSuccess;
+}
+
+}  // namespace
+
+void IndexWork::release() {
+  for (auto*& p : k) { if (p) (void)hipFree(p); p = nullptr; }
+  for (auto*& p : v) { if (p) (void)hipFree(p); p = nullptr; }
+  for (auto*& p : u) { if (p) (void)hipFree(p); p = nullptr; }
+  for (auto*& p : sk) { if (p) (void)hipFree(p); p = nullptr; }
+  for (auto*& p : sv) { if (p) (void)hipFree(p); p = nullptr; }
+  if (seg) (void)hipFree(seg);
+  if (flag) (void)hipFree(flag);
+  if (tmp) (void)hipFree(tmp);
+  if (d) (void)hipFree(d);
+  if (h) (void)hipHostFree(h);
+  seg = nullptr;
+  flag = nullptr;
+  tmp = nullptr;
+  d = nullptr;
+  h = nullptr;
+  tmp_bytes = 0;
+  cap = 0;
+}
+
+hipError_t index_alive(IndexWork& w, const uint8_t* alive, uint64_t n, uint32_t* out, uint64_t* m, hipStream_t s) {
+  if (n >= (1ull << 31)) return hipErrorInvalidValue;
+  ITRY(reserve(w, n));
+  *m = 0;
+  if (n == 0) return hipSuccess;
+  ITRY(cub_at(w, s, __LINE__, [&](void* t, size_t& b) {
+    return hipcub::DeviceSelect::Flagged(t, b, hipcub::CountingInputIterator<uint32_t>(0), alive, out, w.d, (int)n, s);
+  }));
+  ITRY(fetch(w, 1, s));
+  *m = w.h[0];
+  return hipSuccess;
+}
+
+hipError_t index_select(IndexWork& w, const uint64_t* lo, const uint64_t* hi, const int64_t* ts,
+                        const uint8_t* alive, uint64_t n, int mode, uint32_t* perm, uint64_t* off,
+                        uint64_t* n_sel, uint64_t* n_traces, hipStream_t s) {
+  uint64_t m = 0;
+  *n_sel = *n_traces = 0;
+  if (n >= (1ull << 31)) return hipErrorInvalidValue;
+  ITRY(reserve(w, n));  // before any w buffer is named: reserve reallocates them
+  ITRY(index_alive(w, alive, n, w.v[0], &m, s));
+  if (m == 0) return hipSuccess;
+  const uint64_t* ts64 = reinterpret_cast<const uint64_t*>(ts);
+  // (low id, timestamp, arrival): timestamp first, then the low id, both stable
+  LAUNCH(k_take, m, ts64, w.v[0], kSign, w.k[0], m);
+  ITRY(sort64(w, w.k[0], w.k[1], w.v[0], w.v[1], m, s));
+  LAUNCH(k_take, m, lo, w.v[1], 0ull, w.k[0], m);
+  uint32_t* const by_key = w.u[3];  // kept for the newest timestamps below
+  ITRY(sort64(w, w.k[0], w.k[1], w.v[1], by_key, m, s));
+  // storage order: (low id, first arrival of the (low id, timestamp) key, arrival)
+  LAUNCH(k_key_heads, m, lo, ts, by_key, m, w.u[0]);
+  ITRY(max_scan(w, w.u[0], w.u[1], m, s));
+  LAUNCH(k_first_seen, m, by_key, w.u[1], m, w.k[0]);
+  ITRY(sort64(w, w.k[0], w.k[1], by_key, w.v[0], m, s));
+  LAUNCH(k_take, m, lo, w.v[0], 0ull, w.k[0], m);
+  ITRY(sort64(w, w.k[0], w.k[1], w.v[0], w.v[1], m, s));
+  uint32_t* const stored = w.v[1];  // low ids ascending, storage order inside; w.k[1] = their low ids
+  uint64_t T = 0;
+  if (mode == SEL_ALL) {
+    ITRY(hipMemcpyAsync(perm, stored, m * 4, hipMemcpyDeviceToDevice, s));
+    LAUNCH(k_runs, m, w.k[1], m, w.flag);
+    ITRY(offsets_of(w, w.flag, m, off, &T, s));
+  } else if (mode == SEL_NEWEST) {
+    LAUNCH(k_runs, m, w.k[1], m, w.flag);
+    ITRY(offsets_of(w, w.flag, m, w.seg, &T, s));  // the same low-id segments in by_key and stored
+    LAUNCH(k_seg_newest, T, w.seg, T, by_key, ts, w.sk[0], w.sv[0]);
+    ITRY(sort64(w, w.sk[0], w.sk[1], w.sv[0], w.sv[1], T, s));
+    LAUNCH(k_seg_sizes, T, w.seg, w.sv[1], T, w.u[0]);
+    ITRY(sum_scan(w, w.u[0], w.u[1], T, false, s));
+    LAUNCH(k_rank_of, T, w.sv[1], T, w.sv[0]);
+    LAUNCH(k_widen, m, w.flag, m, w.u[2]);
+    ITRY(sum_scan(w, w.u[2], w.u[0], m, true, s));
+    LAUNCH(k_place, m, stored, w.u[0], w.seg, w.sv[0], w.u[1], m, perm);
+    LAUNCH(k_new_off, T + 1, w.u[1], T, m, off);
+  } else if (mode == SEL_ALL_STRICT) {
+    // group by (low id, trace id), indexes into `stored` ascending inside; a group goes where
+    // its first span is (first-seen order inside the low id)
+    LAUNCH(k_iota32, m, w.u[0], m);
+    LAUNCH(k_take, m, hi, stored, 0ull, w.k[0], m);
+    ITRY(sort64(w, w.k[0], w.k[1], w.u[0], w.u[1], m, s));
+    LAUNCH(k_take2, m, lo, stored, w.u[1], w.k[0], m);
+    ITRY(sort64(w, w.k[0], w.k[1], w.u[1], w.u[0], m, s));
+    LAUNCH(k_group_heads, m, lo, hi, stored, w.u[0], m, w.u[2]);
+    ITRY(max_scan(w, w.u[2], w.u[1], m, s));
+    LAUNCH(k_group_first, m, w.u[0], w.u[1], m, w.u[2]);
+    ITRY(sort32(w, w.u[2], w.u[1], stored, perm, m, s));
+    LAUNCH(k_trace_heads, m, lo, hi, perm, m, w.flag);
+    ITRY(offsets_of(w, w.flag, m, off, &T, s));
+  } else {
+    return hipErrorInvalidValue;
+  }
+  ITRY(hipStreamSynchronize(s));
+  *n_sel = m;
+  *n_traces = T;
+  return hipSuccess;
+}
+
+hipError_t index_evict(IndexWork& w, const uint64_t* lo, const int64_t* ts, uint8_t* alive, uint64_t n,
+                       uint64_t to_recover, uint64_t* evicted, bool* exhausted, hipStream_t s) {
+  uint64_t m = 0;
+  *evicted = 0;
+  *exhausted = false;
+  if (to_recover == 0) return hipSuccess;
+  if (n >= (1ull << 31)) return hipErrorInvalidValue;
+  ITRY(reserve(w, n));  // before any w buffer is named: reserve reallocates them
+  ITRY(index_alive(w, alive, n, w.v[0], &m, s));
+  if (m == 0) {
+    *exhausted = true;
+    return hipSuccess;
+  }
+  LAUNCH(k_take, m, lo, w.v[0], 0ull, w.k[0], m);
+  ITRY(sort64(w, w.k[0], w.k[1], w.v[0], w.v[1], m, s));
+  LAUNCH(k_runs, m, w.k[1], m, w.flag);
+  uint64_t T = 0;
+  ITRY(offsets_of(w, w.flag, m, w.seg, &T, s));
+  // traces by (smallest timestamp, low id) ascending: the order deleteOldestTrace takes them
+  LAUNCH(k_seg_oldest, T, w.seg, T, w.v[1], ts, w.sk[0], w.sv[0]);
+  ITRY(sort64(w, w.sk[0], w.sk[1], w.sv[0], w.sv[1], T, s));
+  LAUNCH(k_seg_sizes, T, w.seg, w.sv[1], T, w.u[0]);
+  ITRY(sum_scan(w, w.u[0], w.u[1], T, true, s));
+  hipLaunchKernelGGL(k_evict_init, dim3(1), dim3(64), 0, s, T, m, w.d);
+  ITRY(hipGetLastError());
+  LAUNCH(k_evict_find, T, w.u[1], T, to_recover, w.d);
+  LAUNCH(k_rank_of, T, w.sv[1], T, w.sv[0]);
+  LAUNCH(k_widen, m, w.flag, m, w.u[2]);
+  ITRY(sum_scan(w, w.u[2], w.u[0], m, true, s));
+  LAUNCH(k_evict_mark, m, w.v[1], w.u[0], w.sv[0], w.d, m, alive);
+  ITRY(fetch(w, 4, s));
+  *evicted = w.h[2];
+  *exhausted = w.h[3] != 0;
+  return hipSuccess;
+}
+
+}  // namespace zdl

@@ -11,10 +11,11 @@ SpanStore.getDependencies(endTs, lookback) exercises:
 * ``getDependencies(endTs, lookback)`` groups by the low 64 bits of the trace id
   (IMS:323-332, 448-467; strictTraceId is ignored here like the reference), keeps
   the storage order inside a trace (distinct (lowTraceId, timestamp) keys in
-  first-seen order, then insertion order), and hands the engine only the selection
-  (a permutation of the stored spans + CSR offsets: zdl_put_stored gathers on the
-  device) with the QueryRequest.test time window (QueryRequest.java:262-279)
-  evaluated on the device. Returns a single-use Call (Call.java:370-381).
+  first-seen order, then insertion order); eviction, that trace order and the
+  selection are computed on the device (zdl_store_evict / zdl_store_select) and linked
+  there (zdl_put_selection), with the QueryRequest.test time window
+  (QueryRequest.java:262-279) evaluated on the device. Returns a single-use Call
+  (Call.java:370-381).
 """
 from __future__ import annotations
 
@@ -57,17 +58,17 @@ class Call(Generic[T]):
 
 
 class InMemoryStorage:
-    """The span columns live in HBM (a zdl_store, appended once per accept); the host keeps
-    only what eviction and trace order need (low and high trace id, timestamp, alive) in
-    arrays that grow by doubling. A query uploads its selection - a u32 permutation in
-    getDependencies' order + CSR offsets - and the device gathers and links (zdl_put_stored).
-    Evicted spans are released by a device compaction (zdl_store_compact) once they outnumber
-    the live ones, so maxSpanCount bounds the footprint like the reference's."""
+    """The span columns live in HBM (a zdl_store, appended once per accept) with each span's
+    trace id, timestamp and alive byte; the host keeps no per-span state. Eviction
+    (zdl_store_evict) and a query's trace selection (zdl_store_select) run on the device and
+    the selection is gathered and linked there (zdl_put_selection): only counts cross PCIe.
+    Evicted spans are released by a device compaction (zdl_store_compact_evicted) once they
+    outnumber the live ones, so maxSpanCount bounds the footprint like the reference's."""
 
     def __init__(self, strict_trace_id: bool = True, search_enabled: bool = True,
                  max_span_count: int = 500000, device: int = 0, compact_min: int = 1 << 16):
-        """compact_min: evicted spans are released (zdl_store_compact) once they number more
-        than max(live spans, compact_min)."""
+        """compact_min: evicted spans are released once they number more than
+        max(live spans, compact_min)."""
         if max_span_count <= 0:
             raise ValueError("maxSpanCount <= 0")
         self.strict_trace_id = strict_trace_id
@@ -77,12 +78,6 @@ class InMemoryStorage:
         self.compact_min = compact_min
         self._linker = DependencyLinker(device)  # owns the dictionaries
         self._store: Optional[N.Store] = None
-        self._n = 0  # stored spans (alive or evicted, not yet compacted away)
-        self._n_alive = 0
-        self._lo = np.zeros(0, np.uint64)
-        self._hi = np.zeros(0, np.uint64)  # 0 for 64-bit trace ids (normalized 16-char)
-        self._ts = np.zeros(0, np.int64)
-        self._alive = np.zeros(0, bool)
         self._decoder = None  # proto3.Proto3Decoder, created on the first accept_proto3
         self._json_decoder = None  # jsonv2.JsonV2Decoder, created on the first accept_json_v2
 
@@ -92,91 +87,52 @@ class InMemoryStorage:
 
     newBuilder = new_builder
 
-    # -- host index: amortized growth, eviction, compaction ---------------------------------
-    def _append_index(self, lo: np.ndarray, hi: np.ndarray, ts: np.ndarray) -> None:
-        k = len(lo)
-        if self._n + k > len(self._lo):
-            cap = max(self._n + k, 2 * len(self._lo), 1024)
-            for name in ("_lo", "_hi", "_ts", "_alive"):
-                old = getattr(self, name)
-                grown = np.zeros(cap, old.dtype)
-                grown[:self._n] = old[:self._n]
-                setattr(self, name, grown)
-        self._lo[self._n:self._n + k] = lo
-        self._hi[self._n:self._n + k] = hi
-        self._ts[self._n:self._n + k] = ts
-        self._alive[self._n:self._n + k] = True
-        self._n += k
-        self._n_alive += k
+    def _st(self) -> N.Store:
+        if self._store is None:
+            self._store = N.Store(self.device)
+        return self._store
 
-    def _evict(self, to_recover: int):
-        """evictToRecoverSpans / deleteOldestTrace (IMS:184-211): repeatedly the last key of
-        TIMESTAMP_DESCENDING - the smallest timestamp, ties by the smallest lowTraceId - and
-        with it every span of its lowTraceId. One sort per accept: walking the live
-        (timestamp, lowTraceId) keys upwards meets the traces in eviction order."""
+    def _evict(self, incoming: int):
+        """evictToRecoverSpans((stored + incoming) - maxSpanCount) (IMS:156-211) on the device;
+        NoSuchElementException where the reference's TreeMap.lastKey throws (the store ran
+        empty: everything is evicted first, like the reference's loop)."""
+        st = self._st()
+        to_recover = st.alive + incoming - self.max_span_count
         if to_recover <= 0:
             return
-        if self._n_alive == 0:
-            raise NoSuchElementException("evicting from an empty store")
-        idx = np.nonzero(self._alive[:self._n])[0]
-        lo, ts = self._lo[idx], self._ts[idx]
-        order = np.lexsort((lo, ts))
-        ulo, first_at, counts = np.unique(lo, return_index=True, return_counts=True)
-        # traces in the order their smallest key comes up
-        rank = np.empty(len(lo), np.int64)
-        rank[order] = np.arange(len(order))
-        t_first = np.full(len(ulo), np.iinfo(np.int64).max, np.int64)
-        np.minimum.at(t_first, np.searchsorted(ulo, lo), rank)
-        tord = np.argsort(t_first, kind="stable")
-        cum = np.cumsum(counts[tord])
-        k = int(np.searchsorted(cum, to_recover)) + 1  # traces to evict
-        if k > len(ulo):
-            raise NoSuchElementException("evicting from an empty store")
-        victims = ulo[tord[:k]]
-        dead = idx[np.isin(lo, victims)]
-        self._alive[dead] = False
-        self._n_alive -= len(dead)
-        if self._store is not None and self._n - self._n_alive > max(self._n_alive, self.compact_min):
-            self._compact()
-
-    def _compact(self):
-        keep = np.nonzero(self._alive[:self._n])[0]
-        self._store.compact(keep.astype(np.uint32))
-        for name in ("_lo", "_hi", "_ts", "_alive"):
-            setattr(self, name, getattr(self, name)[keep].copy())
-        self._n = self._n_alive = len(keep)
+        try:
+            st.evict(to_recover)
+        except N.ZdlError as e:
+            if e.code == N.ZDL_EREF_NSE:
+                raise NoSuchElementException("evicting from an empty store") from None
+            raise
+        if len(st) - st.alive > max(st.alive, self.compact_min):
+            st.compact_evicted()
 
     def accept(self, spans: Sequence[Span]) -> Call[None]:
         spans = list(spans)
         if spans:  # the reference accepts synchronously inside accept() (IMS:156-181)
-            self._evict((self._n_alive + len(spans)) - self.max_span_count)
+            self._evict(len(spans))
             # one "trace" per span: grouping happens at query time
             cols = pack_traces([[s] for s in spans], self._linker.svc, self._linker.ip4, self._linker.ip6)
-            if self._store is None:
-                self._store = N.Store(self.device)
-            self._store.append(cols)
             hi = np.array([int(s.trace_id[:16], 16) if len(s.trace_id) == 32 else 0 for s in spans], np.uint64)
-            self._append_index(cols.trace_lo, hi, cols.timestamp)
+            self._st().append(cols, hi)
         return Call(lambda: None)
 
     def accept_proto3(self, data: bytes) -> Call[None]:
         """``accept(SpanBytesDecoder.PROTO3.decodeList(data))`` with the decoding on the device
         (zdl_decode_proto3): the decoded columns go from the decoder's HBM
-        buffers into the store without a host round trip; only the low trace ids and
-        timestamps come back for eviction and trace order. Raises
-        ReferenceIllegalArgumentException where the reference's decoder throws. (The
-        strict no-argument getDependencies() needs high trace ids, which this path does not
-        bring back: it groups these spans by their low trace id.)"""
+        buffers into the store without a host round trip. Raises
+        ReferenceIllegalArgumentException where the reference's decoder throws. (The decoder
+        does not keep high trace ids: the strict no-argument getDependencies() groups these
+        spans by their low trace id.)"""
         if self._decoder is None:
             from .proto3 import Proto3Decoder
             self._decoder = Proto3Decoder(self._linker.svc, self._linker.ip4, self._linker.ip6, self.device)
         b = self._decoder.decode(data)
         if b.n_spans:
-            self._evict((self._n_alive + b.n_spans) - self.max_span_count)
-            if self._store is None:
-                self._store = N.Store(self.device)
-            self._store.append_device(b.dev, b.n_spans)
-            self._append_index(b.trace_lo, np.zeros(b.n_spans, np.uint64), b.timestamp)
+            self._evict(b.n_spans)
+            self._st().append_device(b.dev, b.n_spans)
         return Call(lambda: None)
 
     acceptProto3 = accept_proto3
@@ -191,91 +147,28 @@ class InMemoryStorage:
             self._json_decoder = JsonV2Decoder(self._linker.svc, self._linker.ip4, self._linker.ip6, self.device)
         b = self._json_decoder.decode(data)
         if b.n_spans:
-            self._evict((self._n_alive + b.n_spans) - self.max_span_count)
-            if self._store is None:
-                self._store = N.Store(self.device)
-            self._store.append_device(b.dev, b.n_spans)
-            self._append_index(b.trace_lo, np.zeros(b.n_spans, np.uint64), b.timestamp)
+            self._evict(b.n_spans)
+            self._st().append_device(b.dev, b.n_spans)
         return Call(lambda: None)
 
     acceptJsonV2 = accept_json_v2
 
-    # -- trace selections -------------------------------------------------------------------
-    def _storage_order(self, idx):
-        """IMS storage order inside a low trace id (spansByTraceId, IMS:448-454): distinct
-        (lowTraceId, timestamp) keys in first-seen order, then arrival. Returns, per alive span,
-        the first arrival of its key (the sort key before the arrival itself)."""
-        low, ts = self._lo[idx], self._ts[idx]
-        keys = np.stack([low, ts.view(np.uint64)], axis=1)
-        _, inv = np.unique(keys, axis=0, return_inverse=True)
-        inv = inv.reshape(-1)
-        first = np.full(inv.max() + 1, np.iinfo(np.int64).max, np.int64)
-        np.minimum.at(first, inv, np.arange(len(idx), dtype=np.int64))
-        return first[inv]
-
-    def _selection(self):
-        """Alive spans grouped by trace_lo, in getDependencies' trace order: IMS iterates
-        spansByTraceIdTimeStamp in TIMESTAMP_DESCENDING order (timestamp, then lowTraceId,
-        both descending; IMS:272-291, 356-366), so a trace comes at its newest key. Inside a
-        trace: IMS storage order. Returns (store positions, CSR offsets) or None."""
-        idx = np.nonzero(self._alive[:self._n])[0]
-        if len(idx) == 0:
-            return None
-        low = self._lo[idx]
-        ts = self._ts[idx]
-        key_first = self._storage_order(idx)
-        ulow, tinv = np.unique(low, return_inverse=True)
-        newest = np.full(len(ulow), np.iinfo(np.int64).min, np.int64)
-        np.maximum.at(newest, tinv.reshape(-1), ts)
-        newest = newest[tinv.reshape(-1)]
-        order = np.lexsort((np.arange(len(idx)), key_first, ~low, -newest))
-        sel = idx[order]
-        low_sorted = self._lo[sel]
-        starts = np.nonzero(np.concatenate([[True], low_sorted[1:] != low_sorted[:-1]]))[0]
-        offsets = np.concatenate([starts, [len(sel)]]).astype(np.uint64)
-        return sel.astype(np.uint32), offsets
-
-    def _selection_all(self):
-        """getTraces() (IMS:251-262): every alive trace, lowTraceId ascending (TreeMap with
-        STRING_COMPARATOR over normalized 16-hex ids = numeric order), storage order inside;
-        with strictTraceId each split by the full trace id in first-seen order
-        (strictByTraceId, IMS:241-249)."""
-        idx = np.nonzero(self._alive[:self._n])[0]
-        if len(idx) == 0:
-            return None
-        low, hi = self._lo[idx], self._hi[idx]
-        inner = np.lexsort((np.arange(len(idx)), self._storage_order(idx), low))  # storage order per low id
-        rank = np.empty(len(idx), np.int64)
-        rank[inner] = np.arange(len(idx))
-        if self.strict_trace_id:
-            keys = np.stack([low, hi], axis=1)
-            _, ginv = np.unique(keys, axis=0, return_inverse=True)
-            ginv = ginv.reshape(-1)
-            gfirst = np.full(ginv.max() + 1, np.iinfo(np.int64).max, np.int64)
-            np.minimum.at(gfirst, ginv, rank)
-            order = np.lexsort((rank, gfirst[ginv], low))
-        else:
-            order = inner
-        sel = idx[order]
-        a, b = self._lo[sel], self._hi[sel]
-        new = a[1:] != a[:-1]
-        if self.strict_trace_id:
-            new |= b[1:] != b[:-1]
-        starts = np.nonzero(np.concatenate([[True], new]))[0]
-        offsets = np.concatenate([starts, [len(sel)]]).astype(np.uint64)
-        return sel.astype(np.uint32), offsets
-
-    def _link_selection(self, picked, window=None) -> List[DependencyLink]:
-        if picked is None:
+    def _link_selection(self, mode: int, window=None) -> List[DependencyLink]:
+        """Selects on the device (zdl_store_select: getDependencies' trace order for
+        ZDL_SELECT_NEWEST, IMS:272-291, 356-366; getTraces()' for ZDL_SELECT_ALL[_STRICT],
+        IMS:241-262; IMS storage order inside a trace, IMS:448-454) and links the selection."""
+        if self._store is None or self._store.alive == 0:
             return []
-        sel, offsets = picked
+        _, n_traces = self._store.select(mode)
+        if n_traces == 0:
+            return []
         linker = DependencyLinker(self.device)
         linker.svc, linker.ip4, linker.ip6 = self._linker.svc, self._linker.ip4, self._linker.ip6
         try:
             ctx = linker._context()
             if window is not None:
                 ctx.set_window(*window)
-            ctx.put_stored(self._store, sel, offsets)
+            ctx.put_selection(self._store)
             return linker.link()
         finally:
             linker.close()
@@ -287,14 +180,14 @@ class InMemoryStorage:
         getDependencies() (IMS:265-270, used by ZipkinRule): every trace, grouped strictly when
         strictTraceId, returned as a list."""
         if end_ts is None and lookback is None:
-            return self._link_selection(self._selection_all())
+            return self._link_selection(N.ZDL_SELECT_ALL_STRICT if self.strict_trace_id else N.ZDL_SELECT_ALL)
         if end_ts is None or end_ts <= 0:
             raise ValueError("endTs <= 0")
         if lookback is None or lookback <= 0:
             raise ValueError("lookback <= 0")
         if not self.search_enabled:
             return Call(lambda: [])
-        links = self._link_selection(self._selection(), (end_ts, lookback))
+        links = self._link_selection(N.ZDL_SELECT_NEWEST, (end_ts, lookback))
         return Call(lambda: links)
 
     getDependencies = get_dependencies
@@ -302,11 +195,6 @@ class InMemoryStorage:
     def clear(self):
         if self._store is not None:
             self._store.clear()
-        self._n = self._n_alive = 0
-        self._lo = np.zeros(0, np.uint64)
-        self._hi = np.zeros(0, np.uint64)
-        self._ts = np.zeros(0, np.int64)
-        self._alive = np.zeros(0, bool)
 
     def close(self):
         self._linker.close()
