@@ -137,6 +137,44 @@ def json_v2_leg(cols, w, device, doff, links, reps=3):
             "call_spans_per_s": b.n_spans / (cm * 1e-3), "parity": "same links" if got == exp else "MISMATCH"}
 
 
+def store_leg(cols, S, device, links, reps=5):
+    """InMemoryStorage.getDependencies(endTs, lookback) over the batch resident in a zdl_store
+    (IMS:323-332): the device selects the alive spans in getTraces' order
+    (zdl_store_select ZDL_SELECT_NEWEST: radix sorts for storage order and trace order), gathers
+    them and links them under the window (zdl_put_selection); nothing crosses PCIe but counts.
+    The window covers the batch, so the links must equal the columnar path's."""
+    from zipkin_amd import _native as N
+    st = N.Store(device)
+    st.append(cols)
+    ctx = N.Context(S, device=device)
+    end_ms = int(cols.timestamp.max()) // 1000 + 1
+    ctx.set_window(end_ms, end_ms - int(cols.timestamp.min()) // 1000 + 1)
+
+    def query():
+        ctx.reset()
+        st.select(N.ZDL_SELECT_NEWEST)
+        ctx.put_selection(st)
+        return ctx.link()
+
+    got = query()
+    qs, ss = [], []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        query()
+        qs.append(time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        st.select(N.ZDL_SELECT_NEWEST)
+        ss.append(time.perf_counter() - t0)
+    ctx.close()
+    st.close()
+    same = all(np.array_equal(a, b) for a, b in zip(got, links))
+    qm, sm = float(np.median(qs)) * 1e3, float(np.median(ss)) * 1e3
+    return {"spans": cols.n_spans, "get_dependencies_ms": qm, "select_ms": sm,
+            "spans_per_s": cols.n_spans / (qm * 1e-3),
+            "note": "wall clock of select + gather + link + link() download, store resident in HBM",
+            "parity": "same links" if same else "MISMATCH"}
+
+
 def mysql_rows_leg(cols, S, device, max_spans=2_000_000, reps=3):
     """The first traces of the batch (<= max_spans spans) as mysql-v1 cursor rows (one row per
     annotation a span would carry in v1: sr/ca for servers, cs/sa for clients, lc for local spans,
@@ -262,6 +300,7 @@ def main():
     ap.add_argument("--no-proto3", action="store_true", help="skip the proto3 ingest side leg")
     ap.add_argument("--no-mysql-rows", action="store_true", help="skip the mysql-v1 rows side leg")
     ap.add_argument("--no-json", action="store_true", help="skip the JSON v2 ingest side leg")
+    ap.add_argument("--no-store", action="store_true", help="skip the resident-store getDependencies side leg")
     ap.add_argument("--inflight", type=int, default=0,
                     help="steps in flight (contexts used round-robin): default 2 at N = 1, 1 at N > 1")
     ap.add_argument("--no-insertion-order", action="store_true",
@@ -430,6 +469,11 @@ def main():
         log(f"json v2 ingest: {jleg['bytes'] / 1e9:.2f} GB, device {jleg['device_ms']:.2f} ms "
             f"(structure {jleg['structure_ms']:.2f}, spans {jleg['spans_kernel_ms']:.2f}), "
             f"call {jleg['call_ms']:.1f} ms, links {jleg['parity']}")
+    sleg = None
+    if side and not args.no_store:
+        sleg = store_leg(cols, S, local, (p, c, n, e))
+        log(f"store getDependencies: {sleg['get_dependencies_ms']:.2f} ms (select {sleg['select_ms']:.2f} ms), "
+            f"links {sleg['parity']}")
     rows_leg = None
     if side and not args.no_mysql_rows:
         rows_leg = mysql_rows_leg(cols, S, local)
@@ -508,7 +552,8 @@ def main():
                        "step_roofline_frac": bytes_launch / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
                        "k_link_read_frac": read_launch / (tiles * 1e-3) / 1e9 / HBM_PEAK_GBS,
                        "parity": parity, "links": int(len(p)), "insertion_order": ins, "host_buffers": h2d,
-                       "proto3_ingest": p3, "json_v2_ingest": jleg, "mysql_rows": rows_leg},
+                       "proto3_ingest": p3, "json_v2_ingest": jleg, "store_get_dependencies": sleg,
+                       "mysql_rows": rows_leg},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "k_link", "algorithmic_bytes_per_launch": bytes_launch,

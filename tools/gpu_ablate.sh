@@ -6,7 +6,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 TAG=${1:-x}
-B="bench.py --steps 20 --warmup 3 --inflight 1 --no-cpu-baseline --no-parity --no-h2d --no-proto3 --no-json --no-mysql-rows --no-insertion-order"
+B="bench.py --steps 20 --warmup 3 --inflight 1 --no-cpu-baseline --no-parity --no-h2d --no-proto3 --no-json --no-store --no-mysql-rows --no-insertion-order"
 for sk in ${SKIPS:-0 32 64 128 256 512 2048}; do
   ZDL_SKIP=$sk timeout -k 10 100 python -u $B > gpurun_out/abl_${TAG}_$sk.log 2>&1 || exit $?
 done

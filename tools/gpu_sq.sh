@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 O=gpurun_out; mkdir -p $O
 TAG=${1:-sq}
-B="bench.py --steps 3 --warmup 1 --inflight 1 --no-cpu-baseline --no-h2d --no-proto3 --no-json --no-mysql-rows --no-insertion-order --no-parity"
+B="bench.py --steps 3 --warmup 1 --inflight 1 --no-cpu-baseline --no-h2d --no-proto3 --no-json --no-store --no-mysql-rows --no-insertion-order --no-parity"
 P1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"
 P2="SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_SALU SQ_WAIT_ANY SQ_INSTS_SMEM SQ_INSTS_BRANCH"
 for sk in ${SKIPS:-0}; do
