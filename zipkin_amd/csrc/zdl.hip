@@ -1770,7 +1770,13 @@ static hipError_t ensure_map(zdl_ctx* c) {
 }
 
 // Insertion order and daily buckets: k_link only plans (mode 3), k_tail counts every window.
-static bool plan_only_mode(const zdl_ctx* c) { return c->ord || c->days; }
+// k_link mode 3 (every window through k_tail's exact path): daily buckets, tree export, or
+// ZDL_ORD_EXACT=1 (insertion order the PR-1 way, for A/B); mode 4 otherwise on an
+// insertion-order context (simple windows ranked in k_link)
+static bool plan_only_mode(const zdl_ctx* c) {
+  static const bool ord_exact = getenv("ZDL_ORD_EXACT") != nullptr;
+  return c->days || (c->ord && ((c->flags & ZDL_FLAG_TREE_EXPORT) || ord_exact));
+}
 
 // Sparse contexts: the segments (k_link's waves, then k_tail's big traces and queued windows)
 // listed with their start in lg and their link count.
@@ -1859,7 +1865,7 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   if (c->force_tm == TM_HASH && !dense) tm = TM_HASH;
   if (c->force_tm == TM_LOG && SS <= ((size_t)PMAX << PSHIFT) && n_spans < (1ull << 31)) tm = TM_LOG;
   const bool plan_only = plan_only_mode(c);  // k_link mode 3: k_tail counts every window
-  if (plan_only) tm = dense ? TM_DENSE : TM_HASH;
+  if (plan_only || c->ord) tm = dense ? TM_DENSE : TM_HASH;  // (ranks need the table modes)
   if (c->sparse) {  // every link to a log, sorted and merged after k_tail (zdl_sparse.h)
     if (n_spans >= (1ull << 30)) return fail(c, ZDL_EINVAL, "sparse context: a put holds at most 2^30 spans");
     tm = TM_SORT;
@@ -2007,7 +2013,7 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   void* kargs[] = {&A};
   ev_record(c, 0);
   ev_record(c, 1);
-  const int lmode = (c->ord || c->days) ? 3 : (c->prof_on ? 1 : (c->skip ? 2 : 0));
+  const int lmode = plan_only ? 3 : c->ord ? 4 : (c->prof_on ? 1 : (c->skip ? 2 : 0));
   // A failed launch poisons nothing yet either: no kernel of this put ran
   HIP_TRY(c, hipLaunchKernel(k_link_fn(tm, c->window, lmode), dim3(lgrid), dim3(lk::waves(c->window) * 64), kargs,
                              link_block_bytes(lmode == 3 ? 0 : c->window, tm), c->stream));
