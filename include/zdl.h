@@ -250,6 +250,28 @@ int zdl_put_stored(zdl_ctx* ctx, const zdl_store* store, const uint32_t* perm, u
  * not counted), -1 unreachable. n = the last put's span count. Synchronous. */
 int zdl_tree_export(zdl_ctx* ctx, int32_t* node_of, int32_t* parent, int32_t* bfs, uint64_t n);
 
+/* ZDL_FLAG_TREE_EXPORT, the FINE log of DependencyLinker / SpanNode.Builder
+ * (DependencyLinker.java:57-169, SpanNode.java:130, 145-147, 227-231) as codes, per input span i
+ * of the last put (meaningful for node heads, node_of[i] == i): reason[i] = the branch putTrace
+ * took for the node (low 3 bits, ZDL_RSN_NONE for a node the traversal never visits) | flags;
+ * ancestor[i] = head slot of firstRemoteAncestor's span (ZDL_RSN_ANCESTOR), else -1;
+ * link[4i..4i+3] = (parent, child) service ids of the node's link and (parent, child) of the
+ * missing-link backfill (ZDL_RSN_MISSING_LINK), -1 when absent; sorted[i] = the span's position
+ * in its trace after Trace.merge's sort (CLEANUP_COMPARATOR, Trace.java:88-97). Synchronous. */
+#define ZDL_RSN_NONE                0
+#define ZDL_RSN_CLIENT_PARENT       1  /* client span with children: skipped without a message */
+#define ZDL_RSN_NON_REMOTE          2  /* "non remote span; skipping" */
+#define ZDL_RSN_ROOT_CLIENT_UNKNOWN 3  /* "root's client is unknown; skipping" */
+#define ZDL_RSN_MESSAGING           4  /* producer/consumer link */
+#define ZDL_RSN_MESSAGING_NO_BROKER 5  /* "cannot link messaging span to its broker; skipping" */
+#define ZDL_RSN_LINK                6  /* link (after firstRemoteAncestor) */
+#define ZDL_RSN_NO_REMOTE_ANCESTOR  7  /* "cannot find remote ancestor; skipping" */
+#define ZDL_RSN_ANCESTOR            8  /* flag: "found remote ancestor <span>" */
+#define ZDL_RSN_MISSING_LINK       16  /* flag: "detected missing link to client span" + its link */
+#define ZDL_RSN_ERROR              32  /* flag: the node's link is an error link */
+#define ZDL_RSN_ATTRIBUTED         64  /* flag: "attributing span missing parent to root" */
+int zdl_tree_reasons(zdl_ctx* ctx, uint8_t* reason, int32_t* ancestor, int32_t* link, int32_t* sorted, uint64_t n);
+
 /* Waits for the context stream and reports device-side status (e.g. ZDL_EREF_NPE). */
 int zdl_sync(zdl_ctx* ctx);
 

@@ -1,0 +1,102 @@
+"""DependencyLinker(Logger)'s FINE log (DependencyLinker.java:46, 57-169; SpanNode.java:130,
+145-147, 227-231) rendered from the device's reason codes (zdl_tree_reasons): the messages the
+reference's tests assert (DependencyLinkerTest.java:90, 394, and the fake-root / missing-link
+cases; SpanNodeTest's exact builder logs), and the whole message sequence against the oracle's
+restatement on random traces. "processing <span>" / "found remote ancestor <span>" are compared
+by position only: the oracle quotes its own span repr, the facade the first fragment's JSON."""
+import logging
+import random
+
+import pytest
+
+from oracle import dl_oracle as O
+from tests.golden_io import load, spans
+from tests.stress import random_trace
+from zipkin_amd.linker import DependencyLinker
+
+pytestmark = pytest.mark.gpu
+
+DL = load("dependency_linker.json")
+SN = load("span_node.json")
+
+
+class _Capture(logging.Handler):
+    def __init__(self):
+        super().__init__(logging.DEBUG)
+        self.msgs = []
+
+    def emit(self, record):
+        self.msgs.append(record.getMessage())
+
+
+def _logger(name):
+    lg = logging.getLogger(f"zdl.finelog.{name}")
+    lg.setLevel(logging.DEBUG)
+    lg.propagate = False
+    for h in list(lg.handlers):
+        lg.removeHandler(h)
+    cap = _Capture()
+    lg.addHandler(cap)
+    return lg, cap
+
+
+def _device_log(traces, batch=False, name="t"):
+    lg, cap = _logger(name)
+    linker = DependencyLinker(logger=lg)
+    if batch:
+        linker.put_traces(traces)
+    else:
+        for t in traces:
+            linker.put_trace(t)
+    links = linker.link()
+    linker.close()
+    return cap.msgs, links
+
+
+def _shape(msgs):
+    out = []
+    for m in msgs:
+        if m.startswith("processing "):
+            out.append("processing")
+        elif m.startswith("found remote ancestor "):
+            out.append("found remote ancestor")
+        else:
+            out.append(m)
+    return out
+
+
+@pytest.mark.parametrize("case", [c for c in DL["cases"] if c.get("log_contains")], ids=lambda c: c["name"])
+def test_golden_log_messages(case):
+    msgs, _ = _device_log([spans(t) for t in case["traces"]], name=case["name"])
+    for m in case["log_contains"]:
+        assert m in msgs
+
+
+@pytest.mark.parametrize("case", [c for c in SN["cases"] if "log_exact" in c], ids=lambda c: c["name"])
+def test_golden_span_node_builder_log(case):
+    msgs, _ = _device_log([spans(case["spans"])], name=case["name"])
+    assert msgs[:msgs.index("traversing trace tree, breadth-first")] == case["log_exact"]
+
+
+def test_processing_quotes_the_span_json():
+    case = next(c for c in DL["cases"] if c["name"] == "logsTraceId")
+    inputs = spans(case["traces"][0])
+    msgs, _ = _device_log([inputs], name="json")
+    quoted = [m[len("processing "):] for m in msgs if m.startswith("processing ")]
+    assert sorted(quoted) == sorted(s.to_json_v2() for s in inputs)
+
+
+@pytest.mark.parametrize("seed", range(60))
+def test_random_traces_log_sequence_matches_oracle(seed):
+    r = random.Random(91_000 + seed)
+    traces = [random_trace(r, n=r.randint(1, 30), allow_npe=False, id_pool=r.choice([3, 6, 20]))
+              for _ in range(r.randint(1, 6))]
+    traces += [random_trace(r, n=r.randint(65, 140), allow_npe=False, id_pool=60)] if seed % 10 == 0 else []
+    ref_log = []
+    ref = O.DependencyLinker(ref_log)
+    for t in traces:
+        ref.put_trace(t)
+    msgs, links = _device_log(traces, batch=bool(seed % 2), name=f"r{seed}")
+    assert _shape(msgs) == _shape(ref_log)
+    assert [(l.parent, l.child, l.call_count, l.error_count) for l in links] == \
+        [(l.parent, l.child, l.call_count, l.error_count) for l in ref.link()]

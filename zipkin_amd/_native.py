@@ -13,6 +13,9 @@ LIB_PATH = os.environ.get("ZDL_LIB_PATH") or os.path.join(HERE, "libzdl.so")  # 
 
 ZDL_OK, ZDL_EINVAL, ZDL_ENOMEM, ZDL_EDEVICE, ZDL_EREF_NPE, ZDL_EREF_IAE, ZDL_EREF_NSE = 0, -1, -2, -3, -4, -5, -6
 ZDL_SELECT_NEWEST, ZDL_SELECT_ALL, ZDL_SELECT_ALL_STRICT = 0, 1, 2
+(ZDL_RSN_NONE, ZDL_RSN_CLIENT_PARENT, ZDL_RSN_NON_REMOTE, ZDL_RSN_ROOT_CLIENT_UNKNOWN, ZDL_RSN_MESSAGING,
+ ZDL_RSN_MESSAGING_NO_BROKER, ZDL_RSN_LINK, ZDL_RSN_NO_REMOTE_ANCESTOR) = range(8)
+ZDL_RSN_ANCESTOR, ZDL_RSN_MISSING_LINK, ZDL_RSN_ERROR, ZDL_RSN_ATTRIBUTED = 8, 16, 32, 64
 ZDL_DICT_SERVICE, ZDL_DICT_IPV4, ZDL_DICT_IPV6 = 0, 1, 2
 # JSON v2 keys (include/zdl.h): raw service token text, ipv4 text, ipv6 text (missing list only)
 ZDL_DICT_JSON_SERVICE, ZDL_DICT_JSON_IPV4, ZDL_DICT_JSON_IPV6TEXT = 3, 4, 5
@@ -44,7 +47,7 @@ EXPORTS = (
     "zdl_decoder_dict_size", "zdl_decoder_missing", "zdl_decode_proto3", "zdl_decode_proto3_retry",
     "zdl_decoder_download", "zdl_decoder_kernel_ms", "zdl_put_mysql_rows", "zdl_rows_last_error",
     "zdl_comm_unique_id", "zdl_comm_init", "zdl_put_spans_device_multi", "zdl_device_count", "zdl_shard_of",
-    "zdl_tree_export", "zdl_decode_json_v2", "zdl_decode_retry", "zdl_decoder_struct_ms",
+    "zdl_tree_export", "zdl_tree_reasons", "zdl_decode_json_v2", "zdl_decode_retry", "zdl_decoder_struct_ms",
 )
 ZDL_ABI_VERSION = 2
 ZDL_COMM_ID_BYTES = 128
@@ -204,6 +207,8 @@ def lib() -> C.CDLL:
     L.zdl_shard_of.restype = None
     L.zdl_tree_export.argtypes = [vp, vp, vp, vp, u64]
     L.zdl_tree_export.restype = C.c_int
+    L.zdl_tree_reasons.argtypes = [vp, vp, vp, vp, vp, u64]
+    L.zdl_tree_reasons.restype = C.c_int
     if L.zdl_abi_version() != ZDL_ABI_VERSION:
         raise ImportError(f"{LIB_PATH} has ABI {L.zdl_abi_version()}, this binding {ZDL_ABI_VERSION}: rebuild")
     L.zdl_decoder_kernel_ms.restype = C.c_float
@@ -296,6 +301,16 @@ class Context:
         out = [np.empty(n_spans, np.int32) for _ in range(3)]
         self.check(self._L.zdl_tree_export(self.h, *(_ptr(a) for a in out), int(n_spans)))
         return tuple(out)
+
+    def tree_reasons(self, n_spans: int):
+        """ZDL_FLAG_TREE_EXPORT: (reason u8, ancestor i32, link i32 [n, 4], sorted i32) of the last
+        put (zdl_tree_reasons, ZDL_RSN_*)."""
+        reason = np.empty(n_spans, np.uint8)
+        anc = np.empty(n_spans, np.int32)
+        link = np.empty((n_spans, 4), np.int32)
+        srt = np.empty(n_spans, np.int32)
+        self.check(self._L.zdl_tree_reasons(self.h, _ptr(reason), _ptr(anc), _ptr(link), _ptr(srt), int(n_spans)))
+        return reason, anc, link, srt
 
     def device_count(self) -> int:
         return int(self._L.zdl_device_count(self.h))

@@ -145,6 +145,10 @@ struct Args {
   int32_t* tr_node;
   int32_t* tr_parent;
   int32_t* tr_bfs;
+  uint8_t* tr_reason;  // zdl_tree_reasons
+  int32_t* tr_anc;
+  int32_t* tr_link;
+  int32_t* tr_sorted;
   // sparse contexts (zdl_sparse.h): k_tail's links go to log segments in tlg (2 entries per
   // span: at 2 * the trace's / window's first span); tseg_big[bi] / tseg_win[k] = their counts
   int sparse;
@@ -943,6 +947,28 @@ __device__ __forceinline__ void big_exact(const Args& A, uint64_t b, int n, uint
       }
       A.tr_parent[slot] = pr;
       A.tr_bfs[slot] = bf;
+      // reason codes (wave_tree_reasons' encoding): firstRemoteAncestor by walking up
+      const uint32_t sp = v.perm[p];
+      Rsn r{0u, -1, -1, -1, -1};
+      int32_t anc = -1;
+      if (bf >= 0) {
+        int ra = -1;
+        for (int q2 = v.parent[p], st2 = 0; q2 >= 0 && st2 <= n; q2 = v.parent[q2], ++st2)
+          if (kind_of(v.pf[v.perm[q2]]) != ZDL_KIND_NULL) { ra = q2; break; }
+        const bool has = ra >= 0;
+        const uint32_t as = has ? v.perm[ra] : 0u;
+        r = node_reason(v.pf[sp], v.haschild[p] != 0, v.lsvc[sp], v.rsvc[sp], p == rp, has, has ? v.lsvc[as] : -1,
+                        has ? v.pf[as] : 0u, has && v.pid[sp] != 0 && v.pid[sp] == v.id[as]);
+        if (has) anc = (int32_t)(b + as);
+      }
+      if (v.live[p] && !is_shared(v.pf[sp]) && v.pid[sp] == 0 && rp >= 0 && p != rp) r.code |= ZDL_RSN_ATTRIBUTED;
+      A.tr_reason[slot] = (uint8_t)r.code;
+      A.tr_anc[slot] = anc;
+      A.tr_link[4 * slot] = r.pa;
+      A.tr_link[4 * slot + 1] = r.ch;
+      A.tr_link[4 * slot + 2] = r.xpa;
+      A.tr_link[4 * slot + 3] = r.xch;
+      A.tr_sorted[slot] = p;
     }
   }
   for (int p = threadIdx.x; p < n; p += BIG_WG) {
@@ -1356,6 +1382,8 @@ struct zdl_ctx {
   DevBuf<uint64_t> lg_start;
   int force_tm = -1;  // ZDL_TM=hash|dense|log (tests / ablation): k_link's table mode when it fits
   DevBuf<int32_t> tr_node, tr_parent, tr_bfs;  // ZDL_FLAG_TREE_EXPORT: the last put's tree
+  DevBuf<int32_t> tr_anc, tr_link, tr_sorted;  // and its reason codes (zdl_tree_reasons)
+  DevBuf<uint8_t> tr_reason;
   // sparse contexts (zdl_sparse.h): the accumulated links as one list sorted by cell; per put
   // the log segments of k_link and k_tail are gathered (seg_*) into lin and merged
   bool sparse = false;
@@ -1675,6 +1703,7 @@ void zdl_destroy(zdl_ctx* c) {
   c->lg.release(); c->lg_grp.release(); c->lg_n.release(); c->lg_cnt.release(); c->lg_tot.release();
   c->lg_start.release();
   c->tr_node.release(); c->tr_parent.release(); c->tr_bfs.release();
+  c->tr_anc.release(); c->tr_link.release(); c->tr_sorted.release(); c->tr_reason.release();
   c->acc.release(); c->sw.release(); c->seg_src.release(); c->seg_n.release(); c->seg_off.release();
   c->gx_cell.release(); c->gx_call.release(); c->gx_err.release(); c->gx_n.release(); c->gacc.release();
   c->tseg_big.release(); c->tseg_win.release(); c->lin.release(); c->seg_tmp.release();
@@ -2009,9 +2038,21 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
     HIP_TRY(c, hipMemsetAsync(c->tr_node.p, 0xFF, n_spans * 4, c->stream));
     HIP_TRY(c, hipMemsetAsync(c->tr_parent.p, 0xFF, n_spans * 4, c->stream));
     HIP_TRY(c, hipMemsetAsync(c->tr_bfs.p, 0xFF, n_spans * 4, c->stream));
+    HIP_TRY(c, c->tr_reason.ensure(n_spans));
+    HIP_TRY(c, c->tr_anc.ensure(n_spans));
+    HIP_TRY(c, c->tr_link.ensure(4 * n_spans));
+    HIP_TRY(c, c->tr_sorted.ensure(n_spans));
+    HIP_TRY(c, hipMemsetAsync(c->tr_reason.p, 0, n_spans, c->stream));
+    HIP_TRY(c, hipMemsetAsync(c->tr_anc.p, 0xFF, n_spans * 4, c->stream));
+    HIP_TRY(c, hipMemsetAsync(c->tr_link.p, 0xFF, n_spans * 16, c->stream));
+    HIP_TRY(c, hipMemsetAsync(c->tr_sorted.p, 0xFF, n_spans * 4, c->stream));
     A.tr_node = c->tr_node.p;
     A.tr_parent = c->tr_parent.p;
     A.tr_bfs = c->tr_bfs.p;
+    A.tr_reason = c->tr_reason.p;
+    A.tr_anc = c->tr_anc.p;
+    A.tr_link = c->tr_link.p;
+    A.tr_sorted = c->tr_sorted.p;
     c->tr_n = n_spans;
   }
   if (c->ord) {
@@ -3447,6 +3488,20 @@ int zdl_tree_export(zdl_ctx* c, int32_t* node_of, int32_t* parent, int32_t* bfs,
   HIP_TRY(c, hipMemcpy(node_of, c->tr_node.p, n * 4, hipMemcpyDeviceToHost));
   HIP_TRY(c, hipMemcpy(parent, c->tr_parent.p, n * 4, hipMemcpyDeviceToHost));
   HIP_TRY(c, hipMemcpy(bfs, c->tr_bfs.p, n * 4, hipMemcpyDeviceToHost));
+  return ZDL_OK;
+}
+
+int zdl_tree_reasons(zdl_ctx* c, uint8_t* reason, int32_t* ancestor, int32_t* link, int32_t* sorted, uint64_t n) {
+  if (!c || !reason || !ancestor || !link || !sorted) return ZDL_EINVAL;
+  if (!(c->flags & ZDL_FLAG_TREE_EXPORT) || !c->sub.empty()) return fail(c, ZDL_EINVAL, "context without ZDL_FLAG_TREE_EXPORT");
+  if (n != c->tr_n) return fail(c, ZDL_EINVAL, "zdl_tree_reasons: n must be the last put's span count");
+  const int rc = zdl_sync(c);
+  if (rc != ZDL_OK) return rc;
+  if (n == 0) return ZDL_OK;
+  HIP_TRY(c, hipMemcpy(reason, c->tr_reason.p, n, hipMemcpyDeviceToHost));
+  HIP_TRY(c, hipMemcpy(ancestor, c->tr_anc.p, n * 4, hipMemcpyDeviceToHost));
+  HIP_TRY(c, hipMemcpy(link, c->tr_link.p, n * 16, hipMemcpyDeviceToHost));
+  HIP_TRY(c, hipMemcpy(sorted, c->tr_sorted.p, n * 4, hipMemcpyDeviceToHost));
   return ZDL_OK;
 }
 

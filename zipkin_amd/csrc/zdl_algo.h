@@ -374,6 +374,66 @@ __device__ __forceinline__ void link_node(const V& v, int p, int rp, int n, Emit
   if (parent >= 0 && child >= 0) emit(parent, child, is_error, 1);
 }
 
+// ZDL_FLAG_TREE_EXPORT's reason codes (ZDL_RSN_*): the branch DependencyLinker.putTrace takes
+// for one visited node (DependencyLinker.java:58-148), from which the host renders the FINE
+// messages. Restates link_node's decisions without emitting; pid_match = the node's parent id
+// is the ancestor's id (the split-RPC error check, :136-139).
+struct Rsn {
+  uint32_t code;
+  int32_t pa, ch, xpa, xch;
+};
+__device__ __forceinline__ Rsn node_reason(uint32_t pf, bool haschild, int32_t svc, int32_t rsvc, bool is_root,
+                                           bool has_anc, int32_t ran, uint32_t apf, bool pid_match) {
+  Rsn r{0u, -1, -1, -1, -1};
+  uint32_t kind = kind_of(pf);
+  if (kind == ZDL_KIND_CLIENT && haschild) { r.code = ZDL_RSN_CLIENT_PARENT; return r; }
+  if (kind == ZDL_KIND_NULL) {
+    if (svc >= 0 && rsvc >= 0) kind = ZDL_KIND_CLIENT;
+    else { r.code = ZDL_RSN_NON_REMOTE; return r; }
+  }
+  int32_t parent, child;
+  if (kind == ZDL_KIND_SERVER || kind == ZDL_KIND_CONSUMER) {
+    child = svc;
+    parent = rsvc;
+    if (is_root && parent < 0) { r.code = ZDL_RSN_ROOT_CLIENT_UNKNOWN; return r; }
+  } else {
+    parent = svc;
+    child = rsvc;
+  }
+  bool is_error = err_of(pf);
+  if (kind == ZDL_KIND_PRODUCER || kind == ZDL_KIND_CONSUMER) {
+    if (parent >= 0 && child >= 0) {
+      r.code = ZDL_RSN_MESSAGING | (is_error ? ZDL_RSN_ERROR : 0u);
+      r.pa = parent;
+      r.ch = child;
+    } else {
+      r.code = ZDL_RSN_MESSAGING_NO_BROKER;
+    }
+    return r;
+  }
+  uint32_t fl = 0;
+  if (has_anc) {
+    fl |= ZDL_RSN_ANCESTOR;
+    if (ran >= 0) {
+      if (kind == ZDL_KIND_CLIENT && svc >= 0 && ran != svc) {
+        fl |= ZDL_RSN_MISSING_LINK;
+        r.xpa = ran;
+        r.xch = svc;
+      }
+      if (kind == ZDL_KIND_SERVER || parent < 0) parent = ran;
+      if (!is_error && kind_of(apf) == ZDL_KIND_CLIENT && pid_match) is_error = err_of(apf);
+    }
+  }
+  if (parent >= 0 && child >= 0) {
+    r.code = ZDL_RSN_LINK | fl | (is_error ? ZDL_RSN_ERROR : 0u);
+    r.pa = parent;
+    r.ch = child;
+  } else {
+    r.code = ZDL_RSN_NO_REMOTE_ANCESTOR | fl;
+  }
+  return r;
+}
+
 // Insertion order (ZDL_FLAG_INSERTION_ORDER): first[cell] keeps the smallest rank of an
 // addLink of that (parent, child): (put-global position of the trace's first span) << 24
 // | (breadth-first index of the node << 1 | k). The plain load skips the atomic once a

@@ -15,9 +15,18 @@ breadth-first; ZDL_FLAG_INSERTION_ORDER). With
 ``insertion_order=False`` the engine takes its streaming path and ``link()``
 returns the same links sorted by (parent, child) in String order.
 ``merge`` keeps the reference's first-seen order.
+
+``DependencyLinker(logger=...)`` is the package-private ``DependencyLinker(Logger)`` (:46): with
+the logger enabled for DEBUG (java.util.logging FINE), every put takes the exact per-trace path
+with ZDL_FLAG_TREE_EXPORT and the device's reason codes (zdl_tree_reasons) are rendered as the
+reference's FINE messages, in its order (SpanNode.java:130, 145-147, 227-231;
+DependencyLinker.java:57-169). One difference: "processing <span>" and "found remote ancestor
+<span>" quote the node's first fragment in Trace.merge order, not the merged span (the same
+text whenever a node has one fragment).
 """
 from __future__ import annotations
 
+import logging
 from typing import Iterable, List, Optional, Sequence
 
 import numpy as np
@@ -37,9 +46,12 @@ def _capacity(n: int) -> int:
 
 
 class DependencyLinker:
-    def __init__(self, device: int = 0, insertion_order: bool = True):
+    def __init__(self, device: int = 0, insertion_order: bool = True, logger: Optional[logging.Logger] = None):
         self.device = device
-        self.insertion_order = insertion_order
+        self.logger = logger
+        self._fine = logger is not None and logger.isEnabledFor(logging.DEBUG)
+        # the FINE log needs the exact path's tree and reason codes (insertion-order contexts)
+        self.insertion_order = insertion_order or self._fine
         self.svc = Dictionary()
         self.ip4 = Dictionary()
         self.ip6 = Dictionary()
@@ -50,13 +62,13 @@ class DependencyLinker:
     def _context(self) -> N.Context:
         need = _capacity(max(len(self.svc), 1))
         if self._ctx is None:
-            self._ctx = N.Context(need, self.device, insertion_order=self.insertion_order)
+            self._ctx = N.Context(need, self.device, insertion_order=self.insertion_order, tree_export=self._fine)
             self._ranked = (-1, -1, -1)
         elif self._ctx.n_services < need:
             # grow the S x S table: carry the counts (in order) over on the device
             p, c, n, e = self._ctx.link(self._order())
             old = self._ctx
-            self._ctx = N.Context(need, self.device, insertion_order=self.insertion_order)
+            self._ctx = N.Context(need, self.device, insertion_order=self.insertion_order, tree_export=self._fine)
             self._ranked = (-1, -1, -1)
             if len(p):
                 self._ctx.add_links(p, c, n, e)
@@ -86,7 +98,67 @@ class DependencyLinker:
             return self
         cols = pack_traces(traces, self.svc, self.ip4, self.ip6)
         self.put_columns(cols)
+        if self._fine:
+            self._log_put(traces, cols.n_spans)
         return self
+
+    def _log_put(self, traces: Sequence[Sequence[Span]], n: int) -> None:
+        """The last put's FINE messages from the device's tree and reason codes."""
+        node_of, parent, bfs = self._ctx.tree_export(n)
+        reason, anc, link, srt = self._ctx.tree_reasons(n)
+        flat = [s for t in traces for s in t]
+        names = self.svc.strings
+        fine = self.logger.debug
+        base = 0
+        for t in traces:
+            k = len(t)
+            idx = range(base, base + k)
+            by_sort = sorted(idx, key=lambda i: srt[i])
+            # Trace.merge's trace id (Trace.java:34-38): the first input span's, then sorted spans'
+            # while it is not 32 characters; a cleaned span of another length takes it
+            tid = flat[base].trace_id
+            for i in by_sort[1:]:
+                if len(tid) != 32:
+                    tid = flat[i].trace_id
+            cleaned_tid = lambda i: tid if len(flat[i].trace_id) != len(tid) else flat[i].trace_id
+            root_tid = cleaned_tid(by_sort[0])  # SpanNode.Builder's traceId: cleaned.get(0)'s
+            fine(f"building trace tree: traceId={root_tid}")
+            heads = [i for i in by_sort if node_of[i] == i]
+            roots = [i for i in heads if parent[i] == -2]
+            for i in heads:
+                if reason[i] & N.ZDL_RSN_ATTRIBUTED and roots:
+                    fine("attributing span missing parent to root: traceId=%s, rootSpanId=%s, spanId=%s"
+                         % (cleaned_tid(i), flat[roots[0]].id, flat[i].id))
+            if not roots:
+                fine(f"substituting dummy node for missing root span: traceId={root_tid}")
+            fine("traversing trace tree, breadth-first")
+            if not roots:
+                fine("skipping fake root node for broken span tree")
+            for i in sorted((i for i in heads if bfs[i] >= 0), key=lambda i: bfs[i]):
+                fine(f"processing {flat[i].to_json_v2()}")
+                r = int(reason[i])
+                code = r & 7
+                pa, ch, xpa, xch = (int(x) for x in link[i])
+                err = "error " if r & N.ZDL_RSN_ERROR else ""
+                if code == N.ZDL_RSN_NON_REMOTE:
+                    fine("non remote span; skipping")
+                elif code == N.ZDL_RSN_ROOT_CLIENT_UNKNOWN:
+                    fine("root's client is unknown; skipping")
+                elif code == N.ZDL_RSN_MESSAGING_NO_BROKER:
+                    fine("cannot link messaging span to its broker; skipping")
+                elif code == N.ZDL_RSN_MESSAGING:
+                    fine(f"incrementing {err}link {names[pa]} -> {names[ch]}")
+                elif code in (N.ZDL_RSN_LINK, N.ZDL_RSN_NO_REMOTE_ANCESTOR):
+                    if r & N.ZDL_RSN_ANCESTOR:
+                        fine(f"found remote ancestor {flat[anc[i]].to_json_v2()}")
+                    if r & N.ZDL_RSN_MISSING_LINK:
+                        fine("detected missing link to client span")
+                        fine(f"incrementing link {names[xpa]} -> {names[xch]}")
+                    if code == N.ZDL_RSN_LINK:
+                        fine(f"incrementing {err}link {names[pa]} -> {names[ch]}")
+                    else:
+                        fine("cannot find remote ancestor; skipping")
+            base += k
 
     def put_columns(self, cols: Columns) -> "DependencyLinker":
         """Already-packed traces (dictionary ids must come from this linker's dictionaries)."""

@@ -189,6 +189,28 @@ def _norm_endpoint(e: Optional[Endpoint]) -> Optional[Endpoint]:
     return e
 
 
+_ESC = {'"': '\\"', "\\": "\\\\", "\b": "\\b", "\t": "\\t", "\n": "\\n", "\f": "\\f", "\r": "\\r",
+        "\u2028": "\\u2028", "\u2029": "\\u2029"}
+
+
+def _jstr(v: str) -> str:
+    """A quoted JSON string as JsonEscaper.jsonEscape writes it (internal/JsonEscaper.java)."""
+    return '"' + "".join(_ESC.get(c, "\\u%04x" % ord(c) if ord(c) < 0x20 else c) for c in v) + '"'
+
+
+def _endpoint_json(e: "Endpoint") -> str:
+    parts = []
+    if e.service_name is not None:
+        parts.append('"serviceName":' + _jstr(e.service_name))
+    if e.ipv4 is not None:
+        parts.append('"ipv4":"%s"' % e.ipv4)
+    if e.ipv6 is not None:
+        parts.append('"ipv6":"%s"' % e.ipv6)
+    if e.port:
+        parts.append('"port":%d' % e.port)
+    return "{" + ",".join(parts) + "}"
+
+
 @dataclass(frozen=True)
 class Span:
     trace_id: str
@@ -253,6 +275,36 @@ class Span:
     def is_error(self) -> bool:
         """``tags().containsKey("error")`` (DependencyLinker.java:112)."""
         return any(k == "error" for k, _ in self.tags)
+
+    def to_json_v2(self) -> str:
+        """Span.toString(): SpanBytesEncoder.JSON_V2 (internal/V2SpanWriter.java member order,
+        JsonEscaper.jsonEscape). The FINE messages quote spans this way."""
+        out = ['{"traceId":"', self.trace_id, '"']
+        if self.parent_id is not None:
+            out += [',"parentId":"', self.parent_id, '"']
+        out += [',"id":"', self.id, '"']
+        if self.kind is not None:
+            out += [',"kind":"', Kind(self.kind).name, '"']
+        if self.name is not None:
+            out += [',"name":', _jstr(self.name)]
+        if self.timestamp:
+            out.append(',"timestamp":%d' % self.timestamp)
+        if self.duration:
+            out.append(',"duration":%d' % self.duration)
+        for key, ep in (("localEndpoint", self.local_endpoint), ("remoteEndpoint", self.remote_endpoint)):
+            if ep is not None:
+                out += [',"', key, '":', _endpoint_json(ep)]
+        if self.annotations:
+            out.append(',"annotations":[' + ",".join(
+                '{"timestamp":%d,"value":%s}' % (ts, _jstr(v)) for ts, v in self.annotations) + "]")
+        if self.tags:
+            out.append(',"tags":{' + ",".join(_jstr(k) + ":" + _jstr(v) for k, v in self.tags) + "}")
+        if self.debug:
+            out.append(',"debug":true')
+        if self.shared:
+            out.append(',"shared":true')
+        out.append("}")
+        return "".join(out)
 
     @property
     def trace_lo(self) -> str:
