@@ -301,6 +301,8 @@ def main():
     ap.add_argument("--no-mysql-rows", action="store_true", help="skip the mysql-v1 rows side leg")
     ap.add_argument("--no-json", action="store_true", help="skip the JSON v2 ingest side leg")
     ap.add_argument("--no-store", action="store_true", help="skip the resident-store getDependencies side leg")
+    ap.add_argument("--timing-stride", type=int, default=8,
+                    help="k_link HIP events around every n-th put of a context (roofline.achieved)")
     ap.add_argument("--inflight", type=int, default=0,
                     help="steps in flight (contexts used round-robin): default 2 at N = 1, 1 at N > 1")
     ap.add_argument("--no-insertion-order", action="store_true",
@@ -347,7 +349,7 @@ def main():
 
     # HIP events around k_link on every 8th put of the timed region (each event pair costs
     # the step a few microseconds)
-    ctx = N.Context(S, device=local, timing=True, timing_stride=8)
+    ctx = N.Context(S, device=local, timing=True, timing_stride=args.timing_stride)
     combine = "none"
     if world > 1:
         # libzdl joins one RCCL communicator (zdl_comm_init): zdl_link sums every rank's tables
@@ -367,7 +369,8 @@ def main():
     # and launching the next overlaps the GPU's work instead of idling it (~25 us a step at C2).
     # Every step still resets, links every span and reads every link back.
     inflight = args.inflight or (2 if world == 1 else 1)
-    ctxs = [ctx] + [N.Context(S, device=local, timing=True, timing_stride=8) for _ in range(inflight - 1)]
+    ctxs = [ctx] + [N.Context(S, device=local, timing=True, timing_stride=args.timing_stride)
+                    for _ in range(inflight - 1)]
 
     def launch(c):
         c.reset()
