@@ -120,7 +120,6 @@ struct Args {
   // insertion order (ZDL_FLAG_INSERTION_ORDER): first-addLink ranks per cell (ord_min),
   // the put-global position of this put's span 0, and big-trace breadth-first scratch
   unsigned long long* first;
-  unsigned long long* first_wg;  // k_link mode 4 (dense, no window): [cell][workgroup] ranks
   uint64_t span_base;
   // daily buckets (zdl_set_days): rows = days * S (else S), day 0 = midnight day0 (ms);
   // day_first[d] = put-global position of day d's first trace
@@ -1291,27 +1290,6 @@ __global__ void k_merge_compact(const unsigned long long* __restrict__ tcall, co
   ofirst[w] = tfirst[i];
 }
 
-// Insertion order, k_link mode 4 (dense table, no window): every k_link workgroup keeps its
-// first-addLink ranks in LDS and writes them out as one column of first_wg ([cell][workgroup]);
-// one wave per cell folds the columns into first (after k_link, before k_tail on the stream).
-// With one global table instead, the workgroups' atomics on the S x S cells serialized.
-__global__ void k_first_fold(unsigned long long* __restrict__ first, const unsigned long long* __restrict__ first_wg,
-                             uint64_t SS, uint32_t nwg) {
-  const uint64_t cell = (uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (cell >= SS) return;
-  unsigned long long m = ~0ull;
-  for (uint32_t g = (uint32_t)lane; g < nwg; g += 64) {
-    const unsigned long long v = first_wg[cell * nwg + g];
-    m = v < m ? v : m;
-  }
-  for (int d = 32; d >= 1; d >>= 1) {
-    const unsigned long long o = __shfl_xor(m, d, 64);
-    m = o < m ? o : m;
-  }
-  if (lane == 0 && m < first[cell]) first[cell] = m;
-}
-
 }  // namespace zdl
 
 // ====================================================================== host
@@ -1369,7 +1347,7 @@ struct zdl_ctx {
   std::vector<unsigned long long> h_day_first;
   std::vector<int64_t> out_day, out_days;
   DevBuf<unsigned long long> first, o_key;
-  DevBuf<unsigned long long> first_wg;  // insertion order, mode 4: per-k_link-workgroup rank copies
+
   uint64_t span_base = 0;
   DevBuf<uint32_t> o_fa, o_fb, o_bfs;
   // per-put scratch
@@ -1686,7 +1664,7 @@ void zdl_destroy(zdl_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (auto& r : c->rank) r.release();
   c->call.release(); c->errc.release(); c->status.release();
-  c->first.release(); c->first_wg.release(); c->day_first.release(); c->o_key.release(); c->o_fa.release(); c->o_fb.release(); c->o_bfs.release();
+  c->first.release(); c->day_first.release(); c->o_key.release(); c->o_fa.release(); c->o_fb.release(); c->o_bfs.release();
   c->big_list.release(); c->counters.release(); c->retry.release();
   c->cx_win.release();
   if (c->prof_on && c->prof.p) {
@@ -1910,8 +1888,7 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
                           uint64_t n_traces, const uint64_t* n_traces_dev = nullptr) {
   if (c->poisoned) return fail(c, ZDL_EDEVICE, "an earlier put failed between its kernels: call zdl_reset");
   const size_t SS = (size_t)c->rows * c->S;  // table cells (days * S * S with daily buckets)
-  // (insertion order, mode 4: the windowed table size, so that its LDS ranks fit beside it)
-  const int dense = SS <= (size_t)wdense_max(plan_only_mode(c) ? 0 : (c->window || c->ord));
+  const int dense = SS <= (size_t)wdense_max(plan_only_mode(c) ? 0 : c->window);
   // k_link's table mode: dense LDS cells; else the emit log when the partitions fit (S <= 1024,
   // n_spans < 2^31: u32 positions); else the LDS hash with HBM spill
   int tm = dense ? TM_DENSE : (SS <= ((size_t)PMAX << PSHIFT) && n_spans < (1ull << 31) ? TM_LOG : TM_HASH);
@@ -2061,10 +2038,6 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
     HIP_TRY(c, c->o_fb.ensure(n_spans));
     HIP_TRY(c, c->o_bfs.ensure(n_spans));
     A.first = c->first.p;
-    if (!plan_only && !c->window && tm == TM_DENSE) {  // k_link mode 4: LDS ranks, one column each
-      HIP_TRY(c, c->first_wg.ensure((size_t)lgrid * SS));
-      A.first_wg = c->first_wg.p;
-    }
     A.span_base = c->span_base;
     A.o_key = c->o_key.p;
     A.o_fa = c->o_fa.p;
@@ -2087,15 +2060,6 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   HIP_TRY(c, hipLaunchKernel(k_link_fn(tm, c->window, lmode), dim3(lgrid), dim3(lk::waves(c->window, lmode) * 64), kargs,
                              link_block_bytes(lmode == 3 ? 0 : c->window, tm, lmode), c->stream));
   ev_record(c, 7);
-  if (lmode == 4 && A.first_wg) {  // fold the workgroups' rank copies before k_tail ranks
-    hipLaunchKernelGGL(k_first_fold, dim3((unsigned)((SS + 3) / 4)), dim3(256), 0, c->stream, c->first.p,
-                       c->first_wg.p, (uint64_t)SS, (uint32_t)lgrid);
-    const hipError_t fe = hipGetLastError();
-    if (fe != hipSuccess) {
-      c->poisoned = true;
-      return hip_fail(c, fe, "k_first_fold launch");
-    }
-  }
   if (tm == TM_LOG) {  // group the log by partition, count each partition in LDS (zdl_log.inc)
     hipLaunchKernelGGL(k_pscan, dim3(lP), dim3(PSCAN_WG), 0, c->stream, c->lg_cnt.p, lW, lP, c->lg_tot.p);
     hipLaunchKernelGGL(k_pbase, dim3(1), dim3(PMAX), 0, c->stream, c->lg_tot.p, lP, c->lg_tot.p + PMAX);
