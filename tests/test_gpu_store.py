@@ -213,3 +213,32 @@ def test_store_index_link_matches_host_selection():
         assert got == [a.tolist() for a in ctx.link(order=N.ZDL_ORDER_INSERTION)]
         ctx.close()
     st.close()
+
+
+@pytest.mark.parametrize("fmt", ["proto3", "json_v2"])
+@pytest.mark.parametrize("seed", range(6))
+def test_decoded_ingest_evicts_like_accept(fmt, seed):
+    """accept_proto3 / accept_json_v2 (device decode, device columns straight into the store)
+    with the device's eviction at a small maxSpanCount answer getDependencies like the oracle's
+    InMemoryStorage fed the same spans with accept (IMS:156-211)."""
+    from oracle import json_oracle as J
+    from oracle import proto3_oracle as P
+    write = P.write_list if fmt == "proto3" else J.write_list
+    read = (lambda d: P.read_list(d)[0]) if fmt == "proto3" else J.read_list
+    store = InMemoryStorage(max_span_count=60, compact_min=4)
+    ref = O.InMemoryStorage(max_span_count=60)
+    end_ms = (BASE_US + 10_000_000_000) // 1000 + 1000
+    for b in _batches(100 + seed):
+        if len(b) > 60:
+            continue
+        data = write(b)
+        (store.accept_proto3 if fmt == "proto3" else store.accept_json_v2)(data).execute()
+        ref.accept(read(data))  # what the reference's decodeList gives accept
+        try:
+            want = _as_list(ref.get_dependencies(end_ms, 86_400_000 * 2))
+        except O.ReferenceNPE:  # the round trip can null an endpoint: quirk Q1 on both sides
+            with pytest.raises(N.ReferenceNullPointerException):
+                store.get_dependencies(end_ms, 86_400_000 * 2)
+            break
+        assert _as_list(store.get_dependencies(end_ms, 86_400_000 * 2).execute()) == want
+    store.close()
