@@ -375,6 +375,8 @@ typedef struct zdl_decoded {
   const uint64_t* trace_lo;   /* host copies (owned by the decoder) for the storage facade */
   const int64_t*  timestamp;
   uint64_t        n_missing;  /* > 0: bind the keys, then zdl_decode_proto3_retry */
+  const uint64_t* dev_trace_hi; /* device: each span's trace id high 64 bits (0 = 64-bit id), for
+                                   zdl_store_append_traced */
 } zdl_decoded;
 zdl_decoder* zdl_decoder_create(int device);
 void         zdl_decoder_destroy(zdl_decoder* dec);

@@ -242,3 +242,28 @@ def test_decoded_ingest_evicts_like_accept(fmt, seed):
             break
         assert _as_list(store.get_dependencies(end_ms, 86_400_000 * 2).execute()) == want
     store.close()
+
+
+@pytest.mark.parametrize("fmt", ["proto3", "json_v2"])
+@pytest.mark.parametrize("seed", range(6))
+def test_decoded_ingest_strict_no_arg_get_dependencies(fmt, seed):
+    """The decoders keep the trace ids' high 64 bits on the device (zdl_decoded.dev_trace_hi),
+    so getDependencies() with strictTraceId splits decoded spans like accept'ed ones."""
+    from oracle import json_oracle as J
+    from oracle import proto3_oracle as P
+    write = P.write_list if fmt == "proto3" else J.write_list
+    read = (lambda d: P.read_list(d)[0]) if fmt == "proto3" else J.read_list
+    store = InMemoryStorage(strict_trace_id=True, max_span_count=80, compact_min=4)
+    ref = O.InMemoryStorage(strict_trace_id=True, max_span_count=80)
+    for b in _mixed_width_batches(200 + seed):
+        if len(b) > 80:
+            continue
+        data = write(b)
+        (store.accept_proto3 if fmt == "proto3" else store.accept_json_v2)(data).execute()
+        ref.accept(read(data))
+        try:
+            want = _as_list(ref.get_dependencies_all())
+        except O.ReferenceNPE:
+            break
+        assert _as_list(store.get_dependencies()) == want
+    store.close()

@@ -89,7 +89,7 @@ class MysqlRows(C.Structure):
 
 class Decoded(C.Structure):
     _fields_ = [("n_spans", C.c_uint64), ("dev", SpanCols), ("trace_lo", C.POINTER(C.c_uint64)),
-                ("timestamp", C.POINTER(C.c_int64)), ("n_missing", C.c_uint64)]
+                ("timestamp", C.POINTER(C.c_int64)), ("n_missing", C.c_uint64), ("dev_trace_hi", C.c_void_p)]
 
 
 class KernelTimes(C.Structure):
@@ -446,10 +446,10 @@ class Store:
         if rc != ZDL_OK:
             raise ZdlError(rc, self._L.zdl_store_last_error(self.h).decode())
 
-    def append_device(self, dev: SpanCols, n: int) -> None:
+    def append_device(self, dev: SpanCols, n: int, trace_hi: Optional[int] = None) -> None:
         """Appends device columns (e.g. a Decoder's output, trace_lo included) without a host
-        round trip; high trace ids 0."""
-        self._check(self._L.zdl_store_append(self.h, C.byref(dev), int(n)))
+        round trip; trace_hi: device pointer to the high trace ids (None = all 0)."""
+        self._check(self._L.zdl_store_append_traced(self.h, C.byref(dev), trace_hi, int(n)))
 
     def append(self, cols, trace_hi: Optional[np.ndarray] = None) -> None:
         """Appends host columns with their trace ids (trace_hi: high 64 bits, None = 0)."""

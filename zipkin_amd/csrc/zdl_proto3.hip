@@ -79,6 +79,7 @@ struct Out {
   uint32_t* miss_len;  // [4 n]
   unsigned long long* first_err;  // min over failing spans of (span << 1 | (iae ? 1 : 0))
   uint32_t* any_miss;
+  uint64_t* trace_hi;  // the trace id's high 64 bits (0 for a 64-bit id)
 };
 
 enum : int { SLOT_LSVC = 0, SLOT_LIP4 = 1, SLOT_LIP6 = 2, SLOT_RSVC = 3 };
@@ -296,7 +297,7 @@ __global__ void __launch_bounds__(kBlock) k_proto3_spans(const uint8_t* __restri
   Rd r{buf, len, start[i], F_OK, (lds_u8*)win, w0, wn};
   const int64_t end = (int64_t)(r.pos + slen[i]);
   bool has_trace = false, has_id = false, shared = false, error = false;
-  uint64_t lo = 0, id = 0, pid = 0;
+  uint64_t lo = 0, hi = 0, id = 0, pid = 0;
   int64_t ts = 0;
   uint32_t kind = ZDL_KIND_NULL;
   Ep le, re;
@@ -313,6 +314,7 @@ __global__ void __launch_bounds__(kBlock) k_proto3_spans(const uint8_t* __restri
         for (int32_t j = 0; j < m; ++j) zero &= r.at(off + j) == 0;
         if (m > 16 || zero) r.fail = F_IAE;  // length > 32 hex / all zeros
         lo = be_tail(r, off, m);
+        hi = m > 8 ? be_tail(r, off, m - 8) : 0;
         has_trace = true;
         break;
       }
@@ -454,6 +456,7 @@ __global__ void __launch_bounds__(kBlock) k_proto3_spans(const uint8_t* __restri
     if (re.port) pf |= ZDL_PF_RPORT;
   }
   o.trace_lo[i] = lo;
+  o.trace_hi[i] = hi;
   o.id[i] = id;
   o.pid[i] = pid;
   o.lsvc[i] = ls;
@@ -543,7 +546,7 @@ struct zdl_decoder {
   uint64_t len = 0, n = 0;
   int scan_rc = ZDL_OK;  // result of the top-level scan beyond span n (IAE or empty)
   // outputs
-  DBuf<uint64_t> lo, id, pid;
+  DBuf<uint64_t> lo, hi, id, pid;
   DBuf<int32_t> lsvc, rsvc, ip4, ip6;
   DBuf<uint32_t> pf;
   DBuf<int64_t> ts;
@@ -626,7 +629,8 @@ int run_kernel(zdl_decoder* d, zdl_decoded* out) {
     DEC_TRY(d, hipMemsetAsync(d->status.p + 1, 0, 8, s));
     Dict dict{d->slots.p, d->arena.p, d->cap ? d->cap - 1 : 0};
     Out o{d->lo.p,   d->id.p, d->pid.p, d->lsvc.p,     d->rsvc.p,     d->ip4.p,    d->ip6.p,
-          d->pf.p,   d->ts.p, d->miss.p, d->miss_off.p, d->miss_len.p, d->status.p, (uint32_t*)(d->status.p + 1)};
+          d->pf.p,   d->ts.p, d->miss.p, d->miss_off.p, d->miss_len.p, d->status.p, (uint32_t*)(d->status.p + 1),
+          d->hi.p};
     DEC_TRY(d, hipEventRecord(d->ev[0], s));
     if (d->fmt == 1)
       zjs::k_js_spans<<<(unsigned)((n + zjs::kSpanWG - 1) / zjs::kSpanWG), zjs::kSpanWG, 0, s>>>(
@@ -697,6 +701,7 @@ int run_kernel(zdl_decoder* d, zdl_decoded* out) {
   }
   out->dev = zdl_span_cols{d->lo.p, d->id.p, d->pid.p, d->lsvc.p, d->rsvc.p, d->ip4.p, d->ip6.p, d->pf.p, d->ts.p, nullptr};
   out->trace_lo = d->lo_h.p;
+  out->dev_trace_hi = d->hi.p;
   out->timestamp = d->ts_h.p;
   return ZDL_OK;
 }
@@ -812,6 +817,7 @@ int zdl_decode_proto3(zdl_decoder* d, const uint8_t* data, uint64_t len, zdl_dec
     DEC_TRY(d, hipMemcpyAsync(d->start.p, d->start_h.data(), n * 8, hipMemcpyHostToDevice, s));
     DEC_TRY(d, hipMemcpyAsync(d->slen.p, d->slen_h.data(), n * 4, hipMemcpyHostToDevice, s));
     DEC_TRY(d, d->lo.ensure(n));
+    DEC_TRY(d, d->hi.ensure(n));
     DEC_TRY(d, d->id.ensure(n));
     DEC_TRY(d, d->pid.ensure(n));
     DEC_TRY(d, d->lsvc.ensure(n));
@@ -926,6 +932,7 @@ int zdl_decode_json_v2(zdl_decoder* d, const uint8_t* data, uint64_t len, zdl_de
   if (n >= (1ull << 31)) return dfail(d, ZDL_EINVAL, "zdl_decode_json_v2: at most 2^31 spans per batch");
   d->n = n;
   DEC_TRY(d, d->lo.ensure(n));
+  DEC_TRY(d, d->hi.ensure(n));
   DEC_TRY(d, d->id.ensure(n));
   DEC_TRY(d, d->pid.ensure(n));
   DEC_TRY(d, d->lsvc.ensure(n));

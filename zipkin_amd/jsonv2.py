@@ -127,7 +127,7 @@ class JsonV2Decoder:
             return DecodedBatch(0, None, np.zeros(0, np.uint64), np.zeros(0, np.int64))
         lo = np.ctypeslib.as_array(out.trace_lo, (n,)).copy()
         ts = np.ctypeslib.as_array(out.timestamp, (n,)).copy()
-        return DecodedBatch(n, out.dev, lo, ts)
+        return DecodedBatch(n, out.dev, lo, ts, out.dev_trace_hi)
 
     def decode_columns(self, data: bytes) -> Columns:
         """Host columns of one decoded batch, one span per trace (as ``accept`` packs them)."""

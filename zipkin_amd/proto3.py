@@ -26,8 +26,9 @@ from .model import format_ipv6
 class DecodedBatch:
     n_spans: int
     dev: Optional[N.SpanCols]  # device columns owned by the decoder until its next decode
-    trace_lo: np.ndarray       # host copies: what the storage facade keeps per span
+    trace_lo: np.ndarray       # host copies
     timestamp: np.ndarray
+    dev_trace_hi: Optional[int] = None  # device pointer: the trace ids' high 64 bits (0 = 64-bit id)
 
 
 def _key_string(dict_id: int, raw: bytes) -> str:
@@ -58,7 +59,7 @@ class Proto3Decoder:
             return DecodedBatch(0, None, np.zeros(0, np.uint64), np.zeros(0, np.int64))
         lo = np.ctypeslib.as_array(out.trace_lo, (n,)).copy()
         ts = np.ctypeslib.as_array(out.timestamp, (n,)).copy()
-        return DecodedBatch(n, out.dev, lo, ts)
+        return DecodedBatch(n, out.dev, lo, ts, out.dev_trace_hi)
 
     def decode_columns(self, data: bytes) -> Columns:
         """Host columns of one decoded batch, one span per trace (as ``accept`` packs them)."""

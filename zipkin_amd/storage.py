@@ -122,17 +122,16 @@ class InMemoryStorage:
     def accept_proto3(self, data: bytes) -> Call[None]:
         """``accept(SpanBytesDecoder.PROTO3.decodeList(data))`` with the decoding on the device
         (zdl_decode_proto3): the decoded columns go from the decoder's HBM
-        buffers into the store without a host round trip. Raises
-        ReferenceIllegalArgumentException where the reference's decoder throws. (The decoder
-        does not keep high trace ids: the strict no-argument getDependencies() groups these
-        spans by their low trace id.)"""
+        buffers into the store without a host round trip, high trace ids included (the strict
+        no-argument getDependencies() splits by them). Raises ReferenceIllegalArgumentException
+        where the reference's decoder throws."""
         if self._decoder is None:
             from .proto3 import Proto3Decoder
             self._decoder = Proto3Decoder(self._linker.svc, self._linker.ip4, self._linker.ip6, self.device)
         b = self._decoder.decode(data)
         if b.n_spans:
             self._evict(b.n_spans)
-            self._st().append_device(b.dev, b.n_spans)
+            self._st().append_device(b.dev, b.n_spans, b.dev_trace_hi)
         return Call(lambda: None)
 
     acceptProto3 = accept_proto3
@@ -148,7 +147,7 @@ class InMemoryStorage:
         b = self._json_decoder.decode(data)
         if b.n_spans:
             self._evict(b.n_spans)
-            self._st().append_device(b.dev, b.n_spans)
+            self._st().append_device(b.dev, b.n_spans, b.dev_trace_hi)
         return Call(lambda: None)
 
     acceptJsonV2 = accept_json_v2
