@@ -216,6 +216,173 @@ def mysql_rows_leg(cols, S, device, max_spans=2_000_000, reps=3):
             "spans_per_s": m / t, "note": "rows host-resident (PCIe-inclusive), timing only"}
 
 
+def _sorted_links(p, c, n, e):
+    o = np.lexsort((c, p))
+    return p[o], c[o], n[o], e[o]
+
+
+def _same_links(a, b):
+    a, b = _sorted_links(*a), _sorted_links(*b)
+    return len(a[0]) == len(b[0]) and all(np.array_equal(x, y) for x, y in zip(a, b))
+
+
+def _small_bytes(sizes, n_traces):
+    """k_link's algorithmic bytes: 44 B per span of the traces it links (<= 64 spans) + the
+    8-B offset of every trace (it plans its windows from all of them)."""
+    return BYTES_PER_SPAN * int(sizes[sizes <= 64].sum()) + BYTES_PER_TRACE * (n_traces + 1)
+
+
+def c5_leg(device, steps=3, parity=True, threads=16):
+    """BASELINE.json configs[4] (C5: 10 000 services, Zipf(1.1), depth 64, fan-out <= 1000,
+    Pareto(1.2) trace sizes clipped to [1, 200 000]: 81.1M spans / 16M traces) on one GPU, a
+    sparse context (the link list sorted by cell, no S x S table). One step = reset, put of the
+    HBM-resident batch (k_link, k_mid, the giant tier, k_tail, the log's sort/merge), link() into
+    pinned host columns (4.5M links, 107 MB over PCIe). Per phase: HIP events (ZDL_FLAG_TIMING_ALL,
+    the last step), priced at 44 B per span of the traces that phase links."""
+    import torch
+    from zipkin_amd import _native as N
+    from zipkin_amd import synth
+    w = synth.C5
+    t0 = time.time()
+    cols = synth.generate(w)
+    log(f"c5: generated {cols.n_spans} spans / {cols.n_traces} traces in {time.time() - t0:.1f}s")
+    S = w.total_services
+    sizes = np.diff(cols.offsets.astype(np.int64))
+    dev = torch.device("cuda", device)
+    names = ("id", "parent_id", "local_svc", "remote_svc", "local_ip4", "local_ip6", "port_flags")
+    dc = {k: torch.from_numpy(np.ascontiguousarray(getattr(cols, k)).view(
+        np.int64 if getattr(cols, k).dtype.itemsize == 8 else np.int32)).to(dev) for k in names}
+    doff = torch.from_numpy(cols.offsets.view(np.int64)).to(dev)
+    ptrs = {k: v.data_ptr() for k, v in dc.items()}
+    ctx = N.Context(S, device=device, timing_all=True)
+
+    def step():
+        ctx.reset()
+        ctx.put_spans_device(ptrs, cols.n_spans, doff.data_ptr(), cols.n_traces)
+        return ctx.link(copy=False)
+
+    step()
+    ctx.sync()
+    ts, ph = [], []
+    for _ in range(steps):
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        out = step()
+        ts.append(time.perf_counter() - t1)
+        k = ctx.kernel_times()
+        ph.append({"k_link": k.tiles_ms, "k_mid": k.mid_ms, "giant_tier": k.giant_ms, "k_tail": k.big_ms,
+                   "sparse_merge": k.sparse_ms, "link_compact": k.compact_ms})
+    out = tuple(a.copy() for a in out)
+    ctx.close()
+    del dc, doff
+    ms = float(np.median(ts)) * 1e3
+    gmin = int(os.environ.get("ZDL_GIANT_MIN", "2048")) or None
+    gmin = max(gmin, 192) if gmin else None
+    big = sizes > 192
+    giant = (sizes > gmin) & (sizes <= (1 << 20)) if gmin else np.zeros_like(big)
+    spans = {"k_link": int(sizes[sizes <= 64].sum()), "k_mid": int(sizes[(sizes > 64) & ~big].sum()),
+             "giant_tier": int(sizes[giant].sum()), "k_tail": int(sizes[big & ~giant].sum())}
+    algo = {k: BYTES_PER_SPAN * v for k, v in spans.items()}
+    algo["k_link"] = _small_bytes(sizes, cols.n_traces)
+    last = ph[-1]
+    kern = {}
+    for k in ("k_link", "k_mid", "giant_tier", "k_tail"):
+        t = last[k]
+        gbs = algo[k] / (t * 1e-3) / 1e9 if t and t > 0 else None
+        kern[k] = {"ms": t, "spans": spans[k], "algorithmic_bytes": algo[k], "achieved_gbs": gbs,
+                   "frac": gbs / HBM_PEAK_GBS if gbs else None}
+    for k in ("sparse_merge", "link_compact"):
+        kern[k] = {"ms": last[k]}
+    res = {"workload": w.name, "spans": cols.n_spans, "traces": cols.n_traces, "services": S,
+           "ms_per_step": ms, "spans_per_s": cols.n_spans / (ms * 1e-3),
+           "step_roofline_frac": (BYTES_PER_SPAN * cols.n_spans + BYTES_PER_TRACE * (cols.n_traces + 1))
+           / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+           "steps": steps, "giant_min": gmin, "links": int(len(out[0])), "phases": kern,
+           "note": "phase times: HIP events of the last step (the giant tier's include its two host syncs); "
+                   "step: wall clock of reset + put + link() into pinned host columns", "parity": None}
+    if parity:
+        from oracle import ref
+        t1 = time.perf_counter()
+        st, op, oc, on, oe = ref.link(cols, threads=threads)
+        res["parity"] = "bit-exact" if st == 0 and _same_links(out, (op, oc, on, oe)) else "MISMATCH"
+        res["oracle_s"] = time.perf_counter() - t1
+    return res
+
+
+def pmc_probe(config, traces, puts=4):
+    """The dominant kernel alone for the PMC passes (run under rocprofv3 by pmc_traffic): the
+    same batch as the measured step, `puts` puts on a sorted context."""
+    import torch
+    from zipkin_amd import _native as N
+    from zipkin_amd import synth
+    w = synth.CONFIGS[config]
+    if config == "c3":
+        w = w.scaled(C3_TRACES_PER_GPU)
+    if traces:
+        w = w.scaled(traces)
+    cols = synth.generate(w)
+    names = ("id", "parent_id", "local_svc", "remote_svc", "local_ip4", "local_ip6", "port_flags")
+    dev = torch.device("cuda", 0)
+    dc = {k: torch.from_numpy(np.ascontiguousarray(getattr(cols, k)).view(
+        np.int64 if getattr(cols, k).dtype.itemsize == 8 else np.int32)).to(dev) for k in names}
+    doff = torch.from_numpy(cols.offsets.view(np.int64)).to(dev)
+    ctx = N.Context(w.total_services, device=0)
+    for _ in range(puts):
+        ctx.reset()
+        ctx.put_spans_device({k: v.data_ptr() for k, v in dc.items()}, cols.n_spans, doff.data_ptr(), cols.n_traces)
+        ctx.link()
+    ctx.close()
+    print(json.dumps({"n_spans": cols.n_spans, "puts": puts}))
+    return 0
+
+
+def pmc_traffic(config, traces, kernel="k_link<", timeout=150):
+    """roofline.traffic measured for the build that just ran: two rocprofv3 passes over
+    `bench.py --pmc-probe` in child processes (FETCH_SIZE, then WRITE_SIZE: one counter block
+    each), averaged over the probe's launches of the dominant kernel. HBM bytes per launch =
+    2 x FETCH_SIZE + WRITE_SIZE in KiB (the gfx950 FETCH_SIZE correction, MI355X_MICROARCH.md
+    §HBM; calibrated for k_link's 4/8-B lanes, profiles/*_fetch_calibration.json). None if
+    rocprofv3 is missing or a pass fails."""
+    import csv
+    import shutil
+    import signal
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3")
+    if not prof:
+        return None, None
+    vals = {}
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix="zdl_pmc_")
+        cmd = [prof, "--pmc", counter, "-d", d, "-o", "run", "--output-format", "csv", "--",
+               sys.executable, os.path.abspath(__file__), "--pmc-probe", "--config", config]
+        if traces:
+            cmd += ["--traces", str(traces)]
+        p = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, start_new_session=True)
+        try:
+            rc = p.wait(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.wait()
+            log(f"pmc {counter}: timed out")
+            return None, None
+        rows = []
+        for root, _, files in os.walk(d):
+            for f in files:
+                if f.endswith("counter_collection.csv"):
+                    rows += [r for r in csv.DictReader(open(os.path.join(root, f)))
+                             if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter]
+        shutil.rmtree(d, ignore_errors=True)
+        if rc != 0 or not rows:
+            log(f"pmc {counter}: rc {rc}, {len(rows)} rows")
+            return None, None
+        vals[counter] = sum(float(r["Counter_Value"]) for r in rows) / len(rows) * 1024
+    hbm = 2 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]
+    return hbm, {"fetch_size_bytes": vals["FETCH_SIZE"], "write_size_bytes": vals["WRITE_SIZE"],
+                 "how": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over bench.py --pmc-probe (this build, "
+                        "same batch), 2 x FETCH_SIZE + WRITE_SIZE per k_link launch"}
+
+
 def cpu_info():
     """The host cores this process may run on: affinity mask, capped by a cgroup CPU quota
     (the GPU box shares its host: nproc shows the whole machine), plus the CPU model."""
@@ -301,6 +468,10 @@ def main():
     ap.add_argument("--no-mysql-rows", action="store_true", help="skip the mysql-v1 rows side leg")
     ap.add_argument("--no-json", action="store_true", help="skip the JSON v2 ingest side leg")
     ap.add_argument("--no-store", action="store_true", help="skip the resident-store getDependencies side leg")
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5 (high-cardinality) side leg")
+    ap.add_argument("--no-traffic", action="store_true",
+                    help="skip the rocprofv3 FETCH_SIZE / WRITE_SIZE passes behind roofline.traffic")
+    ap.add_argument("--pmc-probe", action="store_true", help=argparse.SUPPRESS)  # child of pmc_traffic
     ap.add_argument("--timing-stride", type=int, default=8,
                     help="k_link HIP events around every n-th put of a context (roofline.achieved)")
     ap.add_argument("--inflight", type=int, default=0,
@@ -308,6 +479,9 @@ def main():
     ap.add_argument("--no-insertion-order", action="store_true",
                     help="skip the side measurement of the insertion-order mode (N = 1 only)")
     args = ap.parse_args()
+
+    if args.pmc_probe:
+        return pmc_probe(args.config or "c2", args.traces)
 
     import torch
 
@@ -321,9 +495,11 @@ def main():
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     dist = None
     if world > 1:
+        # a CPU (gloo) group for the bootstrap only: the RCCL unique id broadcast, barriers and
+        # the max-over-ranks timing. The one communicator on the GPUs is libzdl's own (zdl_comm_init).
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", init_method="env://")
+        dist.init_process_group("gloo", init_method="env://")
     dev = torch.device("cuda", local)
 
     config = args.config or ("c2" if world == 1 else "c3")
@@ -353,17 +529,16 @@ def main():
     combine = "none"
     if world > 1:
         # libzdl joins one RCCL communicator (zdl_comm_init): zdl_link sums every rank's tables
-        # with ncclAllReduce over xGMI inside the library, as a JVM caller would get it
+        # with ncclAllReduce over xGMI inside the library, as a JVM caller would get it. There is
+        # no other combine path: a rank that cannot join fails the run.
         uid = [N.Context.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         try:
             ctx.comm_init(uid[0], rank, world)
-            combine = "libzdl RCCL all-reduce (zdl_comm_init)"
-        except N.ZdlError as ex:  # keep the scaling run alive: the same sum through torch's RCCL
-            log(f"[rank {rank}] zdl_comm_init failed ({ex}); combining through torch.distributed")
-            combine = "torch.distributed all-reduce of exported tables"
-    tcall = torch.zeros(S * S, dtype=torch.int64, device=dev) if combine.startswith("torch") else None
-    terr = torch.zeros(S * S, dtype=torch.int64, device=dev) if combine.startswith("torch") else None
+        except N.ZdlError as ex:
+            log(f"[rank {rank}] zdl_comm_init failed: {ex}")
+            sys.exit(1)
+        combine = "libzdl RCCL all-reduce (zdl_comm_init)"
     # Steps in flight: with 2, step k+1's reset and put (another context, its own stream) are
     # enqueued before step k's links are read, so the host's work of reading one step's links
     # and launching the next overlaps the GPU's work instead of idling it (~25 us a step at C2).
@@ -375,13 +550,6 @@ def main():
     def launch(c):
         c.reset()
         c.put_spans_device(ptrs, cols.n_spans, doff.data_ptr(), cols.n_traces)
-        if tcall is not None:
-            c.table_export(tcall.data_ptr(), terr.data_ptr())
-            c.sync()
-            dist.all_reduce(tcall)
-            dist.all_reduce(terr)
-            torch.cuda.synchronize(dev)
-            c.table_import(tcall.data_ptr(), terr.data_ptr())
 
     def run(k_steps):
         """k_steps steps: every step's put is launched, every step's links are read."""
@@ -389,10 +557,10 @@ def main():
         for k in range(k_steps):
             launch(ctxs[k % inflight])
             if k >= inflight - 1:
-                res = ctxs[(k - inflight + 1) % inflight].link()
+                res = ctxs[(k - inflight + 1) % inflight].link(copy=False)
         for k in range(max(k_steps - inflight + 1, 0), k_steps):
-            res = ctxs[k % inflight].link()
-        return res
+            res = ctxs[k % inflight].link(copy=False)
+        return tuple(a.copy() for a in res)  # views of the context's output columns until its next link
 
     def sync_all():
         for c in ctxs:
@@ -426,10 +594,10 @@ def main():
         sync_all()
         serial_ms = (time.perf_counter() - t1) / ns * 1e3
     if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-        tot = torch.tensor([cols.n_spans], dtype=torch.int64, device=dev)
+        tot = torch.tensor([cols.n_spans], dtype=torch.int64)
         dist.all_reduce(tot)
         total_spans = int(tot.item())
     else:
@@ -486,6 +654,11 @@ def main():
         h2d = h2d_leg(cols, S, local)
         log(f"host buffers: H2D {h2d['h2d_ms']:.2f} ms ({h2d['h2d_gbs']:.1f} GB/s pinned), put+link from pageable "
             f"host columns {h2d['e2e_ms']:.2f} ms")
+    c5 = None
+    if side and not args.no_c5:
+        c5 = c5_leg(local, parity=not args.no_parity, threads=cpu_info()["usable"])
+        log(f"c5: {c5['ms_per_step']:.2f} ms/step ({c5['spans_per_s']:.3e} spans/s), links {c5['parity']}, "
+            + ", ".join(f"{k} {v['ms']:.3f} ms" for k, v in c5["phases"].items() if v["ms"] is not None))
     parity = None
     cpu = None
     if rank == 0 and world == 1 and not args.no_parity:
@@ -524,17 +697,16 @@ def main():
         ms_step = elapsed / args.steps * 1e3
         # every span once (44 B) and every trace offset once
         bytes_launch = BYTES_PER_SPAN * cols.n_spans + BYTES_PER_TRACE * (cols.n_traces + 1)
-        read_launch = READ_BYTES_PER_SPAN * cols.n_spans + BYTES_PER_TRACE * (cols.n_traces + 1)
-        achieved = bytes_launch / (tiles * 1e-3) / 1e9
+        # k_link is priced with the spans it links (traces of <= 64 spans: all of C2's and C3's)
+        sizes = np.diff(cols.offsets.astype(np.int64))
+        klink_bytes = _small_bytes(sizes, cols.n_traces)
+        small = int(sizes[sizes <= 64].sum())
+        read_launch = READ_BYTES_PER_SPAN * small + BYTES_PER_TRACE * (cols.n_traces + 1)
+        achieved = klink_bytes / (tiles * 1e-3) / 1e9
         traffic = None
-        pmc = os.path.join(ROOT, "profiles", "pmc_k_link.json")
-        if os.path.exists(pmc):
-            try:
-                d = json.load(open(pmc))
-                if d.get("workload") == w.name and d.get("n_spans") == cols.n_spans:
-                    traffic = d.get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
+        traffic_src = None
+        if world == 1 and not args.no_traffic:  # PMC passes of this very build, in child processes
+            traffic, traffic_src = pmc_traffic(config, args.traces)
         line = {
             "metric": METRIC,
             "value": total_spans / elapsed * args.steps,
@@ -556,10 +728,10 @@ def main():
                        "k_link_read_frac": read_launch / (tiles * 1e-3) / 1e9 / HBM_PEAK_GBS,
                        "parity": parity, "links": int(len(p)), "insertion_order": ins, "host_buffers": h2d,
                        "proto3_ingest": p3, "json_v2_ingest": jleg, "store_get_dependencies": sleg,
-                       "mysql_rows": rows_leg},
+                       "mysql_rows": rows_leg, "c5": c5},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_link", "algorithmic_bytes_per_launch": bytes_launch,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                         "kernel": "k_link", "algorithmic_bytes_per_launch": klink_bytes,
                          "bytes_per_span": BYTES_PER_SPAN, "bytes_per_trace": BYTES_PER_TRACE},
             "cpu_baseline": cpu,
         }

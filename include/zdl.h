@@ -36,7 +36,8 @@
 extern "C" {
 #endif
 
-#define ZDL_ABI_VERSION 2  /* 2: zdl_config.n_devices / device_ids, RCCL combine */
+#define ZDL_ABI_VERSION 3  /* 2: zdl_config.n_devices / device_ids, RCCL combine; 3: zdl_kernel_times
+                              per phase of a put (mid_ms, giant_ms, sparse_ms) */
 
 /* ---- status codes ---- */
 #define ZDL_OK          0
@@ -146,14 +147,18 @@ typedef struct zdl_links {
   const int64_t* error_count;
 } zdl_links;
 
-typedef struct zdl_kernel_times {
+typedef struct zdl_kernel_times {  /* the last put's phases (ZDL_FLAG_TIMING_ALL) unless noted */
   float plan_ms;     /* unused (0): k_link plans its windows from the offsets itself */
-  float tiles_ms;    /* k_link: every trace of <= 64 spans */
-  float big_ms;      /* k_tail: queued windows, traces > 64 spans, ordered compaction */
-  float reduce_ms;   /* unused (0) */
-  float compact_ms;  /* k_compact (zdl_link) */
+  float tiles_ms;    /* k_link: every trace of <= 64 spans (ZDL_FLAG_TIMING: mean of the puts) */
+  float big_ms;      /* k_tail: queued windows, traces > 64 spans k_mid and the giant tier left,
+                        ordered compaction */
+  float reduce_ms;   /* LOG mode's reduce of k_link's emit log (k_pscan .. k_hist) */
+  float compact_ms;  /* zdl_link's compaction */
   uint32_t n_tiles, n_big, grid;  /* n_tiles: puts averaged into tiles_ms (ZDL_FLAG_TIMING) */
   float full_ms;     /* unused (0): k_tail runs the queued windows */
+  float mid_ms;      /* k_mid: traces of 65..192 spans, one wave each */
+  float giant_ms;    /* the device-wide big-trace tier (sparse contexts), host syncs included */
+  float sparse_ms;   /* sparse contexts: gathering, sorting and merging the put's link log */
 } zdl_kernel_times;
 
 /* Context lifecycle. zdl_create returns NULL on failure (zdl_create_error() says why). */

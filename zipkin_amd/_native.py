@@ -49,7 +49,7 @@ EXPORTS = (
     "zdl_comm_unique_id", "zdl_comm_init", "zdl_put_spans_device_multi", "zdl_device_count", "zdl_shard_of",
     "zdl_tree_export", "zdl_tree_reasons", "zdl_decode_json_v2", "zdl_decode_retry", "zdl_decoder_struct_ms",
 )
-ZDL_ABI_VERSION = 2
+ZDL_ABI_VERSION = 3
 ZDL_COMM_ID_BYTES = 128
 
 
@@ -95,7 +95,8 @@ class Decoded(C.Structure):
 class KernelTimes(C.Structure):
     _fields_ = [("plan_ms", C.c_float), ("tiles_ms", C.c_float), ("big_ms", C.c_float),
                 ("reduce_ms", C.c_float), ("compact_ms", C.c_float), ("n_tiles", C.c_uint32),
-                ("n_big", C.c_uint32), ("grid", C.c_uint32), ("full_ms", C.c_float)]
+                ("n_big", C.c_uint32), ("grid", C.c_uint32), ("full_ms", C.c_float), ("mid_ms", C.c_float),
+                ("giant_ms", C.c_float), ("sparse_ms", C.c_float)]
 
 
 class ZdlError(RuntimeError):
@@ -359,21 +360,24 @@ class Context:
             raise ZdlError(rc, msg)
 
     @staticmethod
-    def _links_to_numpy(out: Links):
+    def _links_to_numpy(out: Links, copy: bool = True):
         n = int(out.n)
         if n == 0:
             z32, z64 = np.zeros(0, np.int32), np.zeros(0, np.int64)
             return z32, z32.copy(), z64, z64.copy()
-        return (np.ctypeslib.as_array(out.parent, (n,)).copy(), np.ctypeslib.as_array(out.child, (n,)).copy(),
-                np.ctypeslib.as_array(out.call_count, (n,)).copy(),
-                np.ctypeslib.as_array(out.error_count, (n,)).copy())
+        cols = (np.ctypeslib.as_array(out.parent, (n,)), np.ctypeslib.as_array(out.child, (n,)),
+                np.ctypeslib.as_array(out.call_count, (n,)), np.ctypeslib.as_array(out.error_count, (n,)))
+        return tuple(a.copy() for a in cols) if copy else cols
 
-    def link(self, order: int = ZDL_ORDER_SORTED):
+    def link(self, order: int = ZDL_ORDER_SORTED, copy: bool = True):
         """(parent, child, call, err) arrays; order ZDL_ORDER_SORTED or, on an
-        insertion_order context, ZDL_ORDER_INSERTION (DependencyLinker.link()'s order)."""
+        insertion_order context, ZDL_ORDER_INSERTION (DependencyLinker.link()'s order).
+        copy=False returns views of the library's output columns (zdl_links: pinned host memory
+        owned by the context), valid until the context's next link/put/close - what a JNI caller
+        reads without a copy."""
         out = Links()
         self.check(self._L.zdl_link(self.h, int(order), C.byref(out)))
-        return self._links_to_numpy(out)
+        return self._links_to_numpy(out, copy)
 
     def set_days(self, day0_ms: int, n_days: int):
         """Daily buckets (zdl_set_days): the timestamp column then holds guessTimestamp."""

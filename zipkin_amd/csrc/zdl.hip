@@ -166,6 +166,9 @@ struct Args {
   uint32_t* retry_count;
   uint32_t* retry;
   uint32_t* ctr_next;  // the next put's counter block, zeroed by this put's k_tail (CTR_* slots)
+  // the device-wide big-trace tier (zdl_giant.inc): per back-list index, 1 = linked there,
+  // 2 = k_tail's exact path, 0 = k_tail as usual; null when the tier did not run
+  const uint8_t* gstat;
 };
 // The counter block of one put (two alternate by put, so no put issues a memset)
 enum : int { CTR_MID = 0, CTR_CX = 1, CTR_LARGE = 2, CTR_TICK_LARGE = 3, CTR_TICK_MID = 4, CTR_RETRY = 5, CTR_N = 8 };
@@ -1081,6 +1084,8 @@ __device__ __forceinline__ void big_one(const Args& A, unsigned char* lds, size_
   big_sync();
 }
 
+#include "zdl_giant.inc"  // the device-wide tier for big traces (sparse contexts)
+
 // ---------------------------------------------------------------- k_compact
 // zdl_link's output record (24 B), copied to the host in one transfer.
 struct ZLink {
@@ -1206,7 +1211,9 @@ __global__ void __launch_bounds__(TAIL_WG, 1) k_tail(Args A) {
       if (j >= nbig) break;
       if (threadIdx.x == 0) sh_j = atomicAdd(A.tick_large, 1u);
       const bool back = j < nlarge;
-      big_one<ORD>(A, lds, tail_block_bytes(WINDOW), back ? A.big_cap - 1u - j : A.retry[j - nlarge], back);
+      const uint32_t bi = back ? A.big_cap - 1u - j : A.retry[j - nlarge];
+      const uint8_t gs = back && A.gstat ? A.gstat[bi] : 0;  // the giant tier's verdict (uniform)
+      if (gs != 1) big_one<ORD>(A, lds, tail_block_bytes(WINDOW), bi, back && gs == 0);
     }
   }
   if (!A.map) return;
@@ -1395,6 +1402,14 @@ struct zdl_ctx {
   DevBuf<int32_t> b_nm;
   DevBuf<unsigned long long> b_hk;
   DevBuf<uint32_t> b_hv;
+  // the device-wide big-trace tier (zdl_giant.inc, sparse contexts): per-put lists and scratch
+  int giant_min = 2048;  // traces longer than this (ZDL_GIANT_MIN; 0: off, k_tail's workgroups)
+  DevBuf<uint32_t> gg_bi, gg_n, gg_tile0, gg_bad, gg_tile_g, gg_bstart, gg_blen, gg_meta, gg_H;
+  DevBuf<uint64_t> gg_base, gg_h0;
+  DevBuf<unsigned long long> gg_root, gg_tsroot, gg_tsmin;
+  DevBuf<int32_t> gg_rootidx;
+  DevBuf<uint8_t> gg_stat;
+  uint32_t* h_gmeta = nullptr;  // pinned: the tier's GM_* words
   int big_exact = 0;
   bool wave_big = true;  // ZDL_WAVE_BIG=0: every big trace takes a workgroup (tests compare both)  // ZDL_BIG_EXACT=1: big traces skip big_simple (tests compare both paths)
   // host-API staging
@@ -1438,7 +1453,7 @@ struct zdl_ctx {
   int window = 0;
   int64_t win_lo = 0, win_hi = 0;
   // timing
-  hipEvent_t ev[8] = {};
+  hipEvent_t ev[12] = {};
   // ZDL_FLAG_TIMING: a ring of (start, end) event pairs around k_link, one pair per put,
   // averaged by zdl_get_kernel_times (no per-put host query)
   static constexpr int LK_RING = 64;
@@ -1509,11 +1524,15 @@ float ev_ms(zdl_ctx* c, int a, int b) {
 
 void put_times(zdl_ctx* c) {
   if (!(c->flags & ZDL_FLAG_TIMING_ALL)) return;
-  c->times.plan_ms = ev_ms(c, 0, 1);
+  // events: 1 | k_link | 7 | LOG reduce | 2 | k_mid | 3 | giant tier | 8 | k_tail | 4 | sparse | 9
+  c->times.plan_ms = 0.f;
+  c->times.full_ms = 0.f;
   c->times.tiles_ms = ev_ms(c, 1, 7);
-  c->times.full_ms = ev_ms(c, 7, 2);
-  c->times.reduce_ms = ev_ms(c, 2, 3);
-  c->times.big_ms = ev_ms(c, 3, 4);
+  c->times.reduce_ms = ev_ms(c, 7, 2);
+  c->times.mid_ms = ev_ms(c, 2, 3);
+  c->times.giant_ms = ev_ms(c, 3, 8);
+  c->times.big_ms = ev_ms(c, 8, 4);
+  c->times.sparse_ms = ev_ms(c, 4, 9);
 }
 
 }  // namespace
@@ -1597,7 +1616,7 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
   if (e == hipSuccess) e = hipMemsetAsync(c->counters.p, 0, (CTR_DONE + 1) * 4, c->stream);
   if (e == hipSuccess) e = hipHostMalloc((void**)&c->h_meta, 16, hipHostMallocDefault);
   // timing-only events: no system-scope fence (cache writeback) between the kernels they bracket
-  for (int i = 0; i < 8 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->ev[i], hipEventDisableSystemFence);
+  for (int i = 0; i < 12 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->ev[i], hipEventDisableSystemFence);
   for (int i = 0; i < 2 * zdl_ctx::LK_RING && e == hipSuccess && (cfg->flags & ZDL_FLAG_TIMING); ++i)
     e = hipEventCreateWithFlags(&c->lk_ev[i & 1][i >> 1], hipEventDisableSystemFence);
   if (e == hipSuccess) {
@@ -1611,10 +1630,12 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
       e = hipFuncSetAttribute(k_link_fn(tm, w), hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)link_block_bytes(w, tm));
     for (int m = 1; m <= 4 && e == hipSuccess; ++m)
-      for (int tm = 0; tm < 2 && e == hipSuccess; ++tm)
+      for (int tm = 0; tm < (m == 4 ? 3 : 2) && e == hipSuccess; ++tm)
         e = hipFuncSetAttribute(k_link_fn(tm, w, m), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)link_block_bytes(m == 3 ? 0 : w, tm, m));
   }
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)k_g_join, hipFuncAttributeMaxDynamicSharedMemorySize, GHCAP * 16);
   for (int d = 0; d < 2 && e == hipSuccess; ++d)
     for (int w = 0; w < 3 && e == hipSuccess; ++w)
       for (int o = 0; o < 2 && e == hipSuccess; ++o)
@@ -1633,6 +1654,9 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
     c->big_exact = be && be[0] == '1';
     const char* wb = getenv("ZDL_WAVE_BIG");
     c->wave_big = !(wb && wb[0] == '0');
+    const char* gm = getenv("ZDL_GIANT_MIN");
+    if (gm) c->giant_min = (int)strtol(gm, nullptr, 0);
+    if (c->giant_min > 0 && c->giant_min < WB_MAX) c->giant_min = WB_MAX;  // k_mid keeps its traces
     const char* ft = getenv("ZDL_TM");
     if (ft) c->force_tm = !strcmp(ft, "hash") ? TM_HASH : (!strcmp(ft, "log") ? TM_LOG : -1);
   }
@@ -1688,6 +1712,12 @@ void zdl_destroy(zdl_ctx* c) {
   c->b_id.release(); c->b_pid.release(); c->b_lsvc.release(); c->b_rsvc.release(); c->b_ip4.release();
   c->b_ip6.release(); c->b_parent.release(); c->b_pf.release(); c->b_perm.release(); c->b_live.release();
   c->b_hasc.release(); c->b_nm.release(); c->b_hk.release(); c->b_hv.release();
+  for (auto* b : {&c->gg_bi, &c->gg_n, &c->gg_tile0, &c->gg_bad, &c->gg_tile_g, &c->gg_bstart, &c->gg_blen,
+                  &c->gg_meta, &c->gg_H})
+    b->release();
+  c->gg_base.release(); c->gg_h0.release(); c->gg_root.release(); c->gg_tsroot.release(); c->gg_tsmin.release();
+  c->gg_rootidx.release(); c->gg_stat.release();
+  if (c->h_gmeta) (void)hipHostFree(c->h_gmeta);
   c->h_id.release(); c->h_pid.release(); c->h_off.release(); c->h_lsvc.release(); c->h_rsvc.release();
   c->h_ip4.release(); c->h_ip6.release(); c->h_pf.release(); c->h_ts.release();
   c->h_lo.release(); c->h_ord.release(); c->grp.release(); c->lw.release();
@@ -1881,6 +1911,77 @@ static int sparse_finish(zdl_ctx* c, uint32_t ep, uint32_t lW, uint64_t n_spans,
   return ZDL_OK;
 }
 
+// The device-wide big-trace tier (zdl_giant.inc) between k_mid and k_tail, sparse contexts only:
+// their put is synchronous anyway (sparse_finish reads its counts), so reading how many traces
+// k_link listed for workgroups, and then the tier's sizes, costs no extra overlap. Sets A.gstat
+// when it ran; k_tail then skips the traces it linked.
+static int giant_run(zdl_ctx* c, Args& A, uint64_t n_spans, uint64_t n_traces) {
+  const hipStream_t s = c->stream;
+  if (!c->h_gmeta) HIP_TRY(c, hipHostMalloc((void**)&c->h_gmeta, GM_WORDS * 4, hipHostMallocDefault));
+  HIP_TRY(c, hipMemcpyAsync(c->h_gmeta, A.large_count, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipStreamSynchronize(s));
+  const uint32_t nl = c->h_gmeta[0];
+  if (nl == 0) return ZDL_OK;
+  if (nl > n_traces) return fail(c, ZDL_EDEVICE, "giant tier: inconsistent big-trace count");
+  const uint64_t ntmax = n_spans / GT + nl + 1;
+  HIP_TRY(c, c->gg_bi.ensure(nl));
+  HIP_TRY(c, c->gg_n.ensure(nl));
+  HIP_TRY(c, c->gg_tile0.ensure(nl));
+  HIP_TRY(c, c->gg_bad.ensure(nl));
+  HIP_TRY(c, c->gg_base.ensure(nl));
+  HIP_TRY(c, c->gg_h0.ensure(nl));
+  HIP_TRY(c, c->gg_root.ensure(nl));
+  HIP_TRY(c, c->gg_tsroot.ensure(nl));
+  HIP_TRY(c, c->gg_tsmin.ensure(nl));
+  HIP_TRY(c, c->gg_rootidx.ensure(nl));
+  HIP_TRY(c, c->gg_stat.ensure(n_traces));
+  HIP_TRY(c, c->gg_tile_g.ensure(ntmax));
+  HIP_TRY(c, c->gg_bstart.ensure(ntmax));
+  HIP_TRY(c, c->gg_blen.ensure(ntmax));
+  HIP_TRY(c, c->gg_meta.ensure(GM_WORDS));
+  GArgs G{};
+  G.bi = c->gg_bi.p;
+  G.base = c->gg_base.p;
+  G.n = c->gg_n.p;
+  G.tile0 = c->gg_tile0.p;
+  G.h0 = c->gg_h0.p;
+  G.root = c->gg_root.p;
+  G.rootidx = c->gg_rootidx.p;
+  G.bad = c->gg_bad.p;
+  G.tsroot = c->gg_tsroot.p;
+  G.tsmin = c->gg_tsmin.p;
+  G.tile_g = c->gg_tile_g.p;
+  G.bstart = c->gg_bstart.p;
+  G.blen = c->gg_blen.p;
+  G.meta = c->gg_meta.p;
+  G.gstat = c->gg_stat.p;
+  G.gmin = (uint32_t)c->giant_min;
+  hipLaunchKernelGGL(k_g_prep, dim3(1), dim3(BIG_WG), 0, s, A, G);
+  HIP_TRY(c, hipGetLastError());
+  HIP_TRY(c, hipMemcpyAsync(c->h_gmeta, c->gg_meta.p, GM_WORDS * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipStreamSynchronize(s));
+  const uint32_t ng = c->h_gmeta[GM_G], nt = c->h_gmeta[GM_NT], maxn = c->h_gmeta[GM_MAXN], nh = c->h_gmeta[GM_NH];
+  A.gstat = c->gg_stat.p;  // every back-list entry has its verdict now (0 when no giant)
+  if (ng == 0) return ZDL_OK;
+  if (nt > ntmax || maxn > (uint32_t)GMAXN) return fail(c, ZDL_EDEVICE, "giant tier: inconsistent sizes");
+  HIP_TRY(c, c->gg_H.ensure(nh));
+  G.H = c->gg_H.p;
+  G.nt = nt;
+  G.per = (nt + 7) / 8;
+  const dim3 tg(8 * G.per), tb(GT);
+  hipLaunchKernelGGL(k_g_hist, tg, tb, 0, s, A, G);
+  hipLaunchKernelGGL(k_g_scan, dim3(std::min<uint32_t>(ng, (uint32_t)c->cus * 4)), dim3(BIG_WG), 0, s, A, G);
+  hipLaunchKernelGGL(k_g_scatter, tg, tb, 0, s, A, G);
+  hipLaunchKernelGGL(k_g_join, tg, tb, GHCAP * 16, s, A, G);
+  hipLaunchKernelGGL(k_g_par, tg, tb, 0, s, A, G);
+  int rounds = 2;  // after r rounds a points 2^r generations up: enough once 2^r >= the depth
+  while (rounds < GROUNDS_MAX && (1u << (rounds - 1)) < maxn) ++rounds;
+  for (int r = 0; r < rounds; ++r) hipLaunchKernelGGL(k_g_jump, tg, tb, 0, s, A, G, r);
+  hipLaunchKernelGGL(k_g_rules, tg, tb, 0, s, A, G);
+  HIP_TRY(c, hipGetLastError());
+  return ZDL_OK;
+}
+
 // Default pipeline: k_link streams every trace of <= WSMALL spans; k_tail re-runs the
 // windows it queued, takes the traces it listed as longer than WSMALL and (small tables)
 // compacts the table into the mapped buffer zdl_link reads.
@@ -1895,7 +1996,9 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   if (c->force_tm == TM_HASH && !dense) tm = TM_HASH;
   if (c->force_tm == TM_LOG && SS <= ((size_t)PMAX << PSHIFT) && n_spans < (1ull << 31)) tm = TM_LOG;
   const bool plan_only = plan_only_mode(c);  // k_link mode 3: k_tail counts every window
-  if (plan_only || c->ord) tm = dense ? TM_DENSE : TM_HASH;  // (ranks need the table modes)
+  // plan-only puts count in k_tail (table modes); insertion-order puts rank every addLink in the
+  // global first-rank table by themselves, so they count in any mode k_link has (LOG included)
+  if (plan_only || (c->ord && tm != TM_LOG)) tm = dense ? TM_DENSE : TM_HASH;
   if (c->sparse) {  // every link to a log, sorted and merged after k_tail (zdl_sparse.h)
     if (n_spans >= (1ull << 30)) return fail(c, ZDL_EINVAL, "sparse context: a put holds at most 2^30 spans");
     tm = TM_SORT;
@@ -1941,7 +2044,8 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   A.cx_win = c->cx_win.p;
   A.skip = c->skip;
   A.prof = c->prof.p;
-  const uint32_t lW = (uint32_t)lgrid * (uint32_t)lk::waves(c->window);
+  const int lmode = plan_only ? 3 : c->ord ? 4 : (c->prof_on ? 1 : (c->skip ? 2 : 0));
+  const uint32_t lW = (uint32_t)lgrid * (uint32_t)lk::waves(c->window, lmode);  // k_link's waves
   const uint32_t lP = (uint32_t)((SS + (1u << PSHIFT) - 1) >> PSHIFT);
   if (tm == TM_SORT) {  // k_link's segments in [0, 2n), k_tail's in [2n, 4n)
     HIP_TRY(c, c->lg.ensure(4 * n_spans));
@@ -2055,7 +2159,6 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   void* kargs[] = {&A};
   ev_record(c, 0);
   ev_record(c, 1);
-  const int lmode = plan_only ? 3 : c->ord ? 4 : (c->prof_on ? 1 : (c->skip ? 2 : 0));
   // A failed launch poisons nothing yet either: no kernel of this put ran
   HIP_TRY(c, hipLaunchKernel(k_link_fn(tm, c->window, lmode), dim3(lgrid), dim3(lk::waves(c->window, lmode) * 64), kargs,
                              link_block_bytes(lmode == 3 ? 0 : c->window, tm, lmode), c->stream));
@@ -2075,7 +2178,6 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
     }
   }
   ev_record(c, 2);
-  ev_record(c, 3);
   c->map_fresh = false;  // k_link has changed the table
   if (A.wb_max) {  // big_list's front (WSMALL < n <= WB_MAX spans): one wave per trace
     hipLaunchKernelGGL(k_mid, dim3((unsigned)c->cus * 4), dim3(MID_WG), 4 * WB_CARVE, c->stream, A);
@@ -2085,6 +2187,15 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
       return hip_fail(c, me, "k_mid launch");
     }
   }
+  ev_record(c, 3);
+  if (c->sparse && c->giant_min > 0 && !c->ord && !c->days) {  // the device-wide big-trace tier
+    const int grc = giant_run(c, A, n_spans, n_traces);
+    if (grc != ZDL_OK) {
+      c->poisoned = true;  // k_link ran: the counter slots hold this put's counts
+      return grc;
+    }
+  }
+  ev_record(c, 8);
   const hipError_t le = hipLaunchKernel(k_tail_fn(c->sparse ? 2 : dense, wmode, c->ord ? 1 : 0), dim3(grid),
                                         dim3(TAIL_WG), kargs, tail_block_bytes(wmode), c->stream);
   if (le != hipSuccess) {
@@ -2094,6 +2205,7 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
     return hip_fail(c, le, "k_tail launch");
   }
   if (A.map) c->seq = A.seq;
+  ev_record(c, 4);
   if (c->sparse) {  // gather the put's log segments, sort, reduce and merge into the list
     const int rc = sparse_finish(c, ep, lW, n_spans, n_traces, off);
     if (rc != ZDL_OK) {
@@ -2104,7 +2216,7 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
     }
   }
   c->span_base += n_spans;  // the next put's traces come after this one's
-  ev_record(c, 4);
+  ev_record(c, 9);
   ++c->epoch;  // k_tail zeroed the other counter slots
   c->map_fresh = A.map != nullptr;
   c->times.grid = (uint32_t)grid;
@@ -2788,10 +2900,12 @@ static int link_sparse(zdl_ctx* c, zdl_links* out, const SparseTable* tab = null
   int rc = ensure_rec(c, m);
   if (rc != ZDL_OK) return rc;
   const size_t cap = c->h_rec_cap;
+  ev_record(c, 5);
   HIP_TRY(c, compact_sparse(c->lw, t.cell, t.call, t.err, m, c->S,
                             c->nrank[0] ? c->rank[0].p : nullptr, c->nrank[0], (int32_t*)c->d_rec,
                             (int32_t*)(c->d_rec + 4 * cap), (int64_t*)(c->d_rec + 8 * cap),
                             (int64_t*)(c->d_rec + 16 * cap), c->stream));
+  ev_record(c, 6);
   HIP_TRY(c, hipMemcpyAsync(c->h_meta, c->status.p, 16, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   rc = status_code(c, (uint32_t)c->h_meta[0]);
@@ -3116,6 +3230,12 @@ int zdl_get_kernel_times(zdl_ctx* c, zdl_kernel_times* out) {
     c->times.tiles_ms = (float)(sum / k);
     c->times.n_tiles = k;  // the puts averaged
     c->lk_n = 0;
+  }
+  if (c->flags & ZDL_FLAG_TIMING_ALL) {  // the last put's and link's phases
+    HIP_TRY(c, enter(c));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    put_times(c);
+    c->times.compact_ms = ev_ms(c, 5, 6);
   }
   *out = c->times;
   return ZDL_OK;

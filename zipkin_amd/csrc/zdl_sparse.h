@@ -43,6 +43,8 @@ struct SparseWork {
   SparseTable next;  // the merged list (swapped with the context's)
   uint64_t* d_count = nullptr;
   uint64_t* h_count = nullptr;  // pinned
+  uint32_t* idx_sorted = nullptr;  // sparse_add: the cells' sort permutation
+  size_t idx_cap = 0;
   void release();
 };
 

@@ -30,8 +30,10 @@ hipError_t grow(T*& p, size_t& cap, size_t n) {
 struct CellOf {
   __host__ __device__ uint32_t operator()(uint32_t k) const { return k >> 1; }
 };
-struct ErrOf {
-  __host__ __device__ unsigned long long operator()(uint32_t k) const { return k & 1u; }
+// one log entry as (call 1 << 32 | error bit): a single reduce by key sums both counts (a put
+// holds < 2^31 entries, so neither half overflows)
+struct PackOf {
+  __host__ __device__ unsigned long long operator()(uint32_t k) const { return (1ull << 32) | (k & 1u); }
 };
 struct Gather {
   const unsigned long long* v;
@@ -39,10 +41,18 @@ struct Gather {
 };
 
 using CellIt = hipcub::TransformInputIterator<uint32_t, CellOf, const uint32_t*>;
-using ErrIt = hipcub::TransformInputIterator<unsigned long long, ErrOf, const uint32_t*>;
-using OneIt = hipcub::ConstantInputIterator<unsigned long long>;
+using PackIt = hipcub::TransformInputIterator<unsigned long long, PackOf, const uint32_t*>;
 using GatherIt = hipcub::TransformInputIterator<unsigned long long, Gather, const uint32_t*>;
 using IdxIt = hipcub::CountingInputIterator<uint32_t>;
+
+// (call << 32 | err) -> call, err (in place for call)
+__global__ void k_unpack(unsigned long long* call, unsigned long long* err, const uint64_t* n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= *n) return;
+  const unsigned long long v = call[i];
+  call[i] = v >> 32;
+  err[i] = v & 0xFFFFFFFFull;
+}
 
 __global__ void k_iota32(uint32_t* p, uint64_t n) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -146,7 +156,7 @@ void SparseTable::release() {
 
 void SparseWork::release() {
   for (void* p : {(void*)tmp, (void*)keys, (void*)bcell, (void*)bcall, (void*)berr, (void*)mcell, (void*)midx,
-                  (void*)vcall, (void*)verr, (void*)d_count})
+                  (void*)vcall, (void*)verr, (void*)d_count, (void*)idx_sorted})
     if (p) (void)hipFree(p);
   if (h_count) (void)hipHostFree(h_count);
   tmp = nullptr;
@@ -160,7 +170,8 @@ void SparseWork::release() {
   verr = nullptr;
   d_count = nullptr;
   h_count = nullptr;
-  tmp_bytes = keys_cap = b_cap = m_cap = 0;
+  idx_sorted = nullptr;
+  tmp_bytes = keys_cap = b_cap = m_cap = idx_cap = 0;
   next.release();
 }
 
@@ -179,17 +190,16 @@ hipError_t sparse_accumulate(SparseWork& w, SparseTable& t, uint32_t* log, uint6
   w.b_cap = std::min(b1, std::min(b2, b3));
   size_t a = 0, b = 0;
   STRY(hipcub::DeviceRadixSort::SortKeys(nullptr, a, log, w.keys, (int)E, 0, key_bits, s));
-  STRY(hipcub::DeviceReduce::ReduceByKey(nullptr, b, CellIt(w.keys, CellOf{}), w.bcell, OneIt(1ull), w.bcall,
-                                         w.d_count, hipcub::Sum(), (int)E, s));
+  STRY(hipcub::DeviceReduce::ReduceByKey(nullptr, b, CellIt(w.keys, CellOf{}), w.bcell, PackIt(w.keys, PackOf{}),
+                                         w.bcall, w.d_count, hipcub::Sum(), (int)E, s));
   STRY(scratch(w, std::max(a, b)));
   size_t bytes = w.tmp_bytes;
   STRY(hipcub::DeviceRadixSort::SortKeys(w.tmp, bytes, log, w.keys, (int)E, 0, key_bits, s));
-  bytes = w.tmp_bytes;  // per cell: call = entries, error = odd entries
-  STRY(hipcub::DeviceReduce::ReduceByKey(w.tmp, bytes, CellIt(w.keys, CellOf{}), w.bcell, OneIt(1ull), w.bcall,
-                                         w.d_count, hipcub::Sum(), (int)E, s));
-  bytes = w.tmp_bytes;
-  STRY(hipcub::DeviceReduce::ReduceByKey(w.tmp, bytes, CellIt(w.keys, CellOf{}), w.bcell, ErrIt(w.keys, ErrOf{}),
-                                         w.berr, w.d_count, hipcub::Sum(), (int)E, s));
+  bytes = w.tmp_bytes;  // per cell: call = entries, error = odd entries, in one pass
+  STRY(hipcub::DeviceReduce::ReduceByKey(w.tmp, bytes, CellIt(w.keys, CellOf{}), w.bcell, PackIt(w.keys, PackOf{}),
+                                         w.bcall, w.d_count, hipcub::Sum(), (int)E, s));
+  hipLaunchKernelGGL(k_unpack, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, w.bcall, w.berr, w.d_count);
+  STRY(hipGetLastError());
   uint64_t U = 0;
   STRY(read_count(w, s, &U));
   return merge_into(w, t, w.bcell, w.bcall, w.berr, U, s);
@@ -209,9 +219,10 @@ hipError_t sparse_add(SparseWork& w, SparseTable& t, const uint32_t* cells, cons
   STRY(grow(w.berr, b3, n));
   w.b_cap = std::min(b1 / 2, std::min(b2, b3));
   uint32_t* idx = w.bcell + n;  // scratch: iota, sorted by cell into keys' partner
-  uint32_t* idx_sorted = nullptr;
-  size_t icap = 0;
-  STRY(grow(idx_sorted, icap, n));
+  size_t icap = w.idx_cap;
+  STRY(grow(w.idx_sorted, icap, n));  // kept in the work area: no allocation per combine, no leak
+  w.idx_cap = icap;
+  uint32_t* idx_sorted = w.idx_sorted;
   hipLaunchKernelGGL(k_iota32, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, idx, n);
   STRY(hipGetLastError());
   size_t a = 0, b = 0;
@@ -234,9 +245,7 @@ hipError_t sparse_add(SparseWork& w, SparseTable& t, const uint32_t* cells, cons
                                          GatherIt(idx_sorted, Gather{err}), w.berr, w.d_count, hipcub::Sum(),
                                          (int)n, s));
   uint64_t U = 0;
-  const hipError_t e = read_count(w, s, &U);
-  (void)hipFree(idx_sorted);
-  STRY(e);
+  STRY(read_count(w, s, &U));
   return merge_into(w, t, w.bcell, w.bcall, w.berr, U, s);
 }
 

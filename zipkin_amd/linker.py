@@ -35,11 +35,18 @@ from . import _native as N
 from .columnar import Columns, Dictionary, pack_traces
 from .model import DependencyLink, Span
 
-MIN_SERVICES = 48  # S*S <= 2560 keeps the engine on its dense LDS table (WDENSE_MAX)
+DENSE_MAX = 67         # S*S <= 4544 (WDENSE_MAX): k_link counts in its dense LDS table
+DENSE_MAX_WINDOW = 50  # S*S <= 2560 (WDENSE_MAX_WINDOW): the same with a time window
 
 
-def _capacity(n: int) -> int:
-    cap = MIN_SERVICES
+def _capacity(n: int, window: bool = False) -> int:
+    """The context's service capacity for n services: the dense table while it fits, then
+    powers of two (up to 1024: k_link's LOG mode, sorted and insertion order; above: a sparse
+    list when sorted, the LDS hash when ranked)."""
+    d = DENSE_MAX_WINDOW if window else DENSE_MAX
+    if n <= d:
+        return d
+    cap = 128
     while cap < n:
         cap *= 2
     return cap
@@ -59,8 +66,8 @@ class DependencyLinker:
         self._ranked = (-1, -1, -1)
 
     # -- context management -------------------------------------------------
-    def _context(self) -> N.Context:
-        need = _capacity(max(len(self.svc), 1))
+    def _context(self, window: bool = False) -> N.Context:
+        need = _capacity(max(len(self.svc), 1), window)
         if self._ctx is None:
             self._ctx = N.Context(need, self.device, insertion_order=self.insertion_order, tree_export=self._fine)
             self._ranked = (-1, -1, -1)

@@ -164,7 +164,7 @@ class InMemoryStorage:
         linker = DependencyLinker(self.device)
         linker.svc, linker.ip4, linker.ip6 = self._linker.svc, self._linker.ip4, self._linker.ip6
         try:
-            ctx = linker._context()
+            ctx = linker._context(window is not None)
             if window is not None:
                 ctx.set_window(*window)
             ctx.put_selection(self._store)
@@ -186,7 +186,16 @@ class InMemoryStorage:
             raise ValueError("lookback <= 0")
         if not self.search_enabled:
             return Call(lambda: [])
-        links = self._link_selection(N.ZDL_SELECT_NEWEST, (end_ts, lookback))
+        # the selection is the snapshot taken now (getTraces(request, false)); LinkDependencies
+        # is a Call.map, so a reference exception (quirk Q1) comes out of execute() (IMS:331-348)
+        try:
+            links = self._link_selection(N.ZDL_SELECT_NEWEST, (end_ts, lookback))
+        except (N.ReferenceNullPointerException, N.ReferenceIllegalArgumentException) as ex:
+            err = ex
+
+            def fail():
+                raise err
+            return Call(fail)
         return Call(lambda: links)
 
     getDependencies = get_dependencies
