@@ -137,18 +137,27 @@ def json_v2_leg(cols, w, device, doff, links, reps=3):
             "call_spans_per_s": b.n_spans / (cm * 1e-3), "parity": "same links" if got == exp else "MISMATCH"}
 
 
-def store_leg(cols, S, device, links, reps=5):
+def store_leg(cols, S, device, links, names, reps=5):
     """InMemoryStorage.getDependencies(endTs, lookback) over the batch resident in a zdl_store
-    (IMS:323-332): the device selects the alive spans in getTraces' order
-    (zdl_store_select ZDL_SELECT_NEWEST: radix sorts for storage order and trace order), gathers
-    them and links them under the window (zdl_put_selection); nothing crosses PCIe but counts.
-    The window covers the batch, so the links must equal the columnar path's."""
+    (IMS:323-332). accept appends the columns to HBM and merges the batch into the
+    store's resident trace index (zdl_store_index.h: radix sorts of the batch + merges, the
+    reference's TreeMap inserts at accept); a query filters the alive spans of that index,
+    orders the traces newest first (one sort of a key per trace), gathers and links them under
+    the window (zdl_put_selection); nothing crosses PCIe but counts and the links. Timed two
+    ways: the raw context (sorted output) and the InMemoryStorage facade exactly as shipped
+    (insertion-order DependencyLinker context sized by _capacity for a window, service ranks,
+    DependencyLink objects out), with the facade's store holding the same columns. The window
+    covers the batch, so the links must equal the columnar path's."""
     from zipkin_amd import _native as N
+    from zipkin_amd.storage import InMemoryStorage
     st = N.Store(device)
+    t0 = time.perf_counter()
     st.append(cols)
+    accept_ms = (time.perf_counter() - t0) * 1e3
     ctx = N.Context(S, device=device)
     end_ms = int(cols.timestamp.max()) // 1000 + 1
-    ctx.set_window(end_ms, end_ms - int(cols.timestamp.min()) // 1000 + 1)
+    lookback = end_ms - int(cols.timestamp.min()) // 1000 + 1
+    ctx.set_window(end_ms, lookback)
 
     def query():
         ctx.reset()
@@ -168,11 +177,28 @@ def store_leg(cols, S, device, links, reps=5):
     ctx.close()
     st.close()
     same = all(np.array_equal(a, b) for a, b in zip(got, links))
-    qm, sm = float(np.median(qs)) * 1e3, float(np.median(ss)) * 1e3
-    return {"spans": cols.n_spans, "get_dependencies_ms": qm, "select_ms": sm,
-            "spans_per_s": cols.n_spans / (qm * 1e-3),
-            "note": "wall clock of select + gather + link + link() download, store resident in HBM",
-            "parity": "same links" if same else "MISMATCH"}
+    # the facade as shipped: its own store (the same columns appended), its dictionary
+    ims = InMemoryStorage(max_span_count=max(cols.n_spans, 500000), device=device)
+    for nm in names:
+        ims._linker.svc.id(nm)
+    ims._st().append(cols)
+    fl = ims.get_dependencies(end_ms, lookback).execute()
+    fs = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        ims.get_dependencies(end_ms, lookback).execute()
+        fs.append(time.perf_counter() - t0)
+    ims.close()
+    p, c, n, e = links
+    exp = sorted(zip((names[i] for i in p.tolist()), (names[i] for i in c.tolist()), n.tolist(), e.tolist()))
+    fsame = sorted((l.parent, l.child, l.call_count, l.error_count) for l in fl) == exp
+    qm, sm, fm = float(np.median(qs)) * 1e3, float(np.median(ss)) * 1e3, float(np.median(fs)) * 1e3
+    return {"spans": cols.n_spans, "accept_ms": accept_ms, "get_dependencies_ms": qm, "select_ms": sm,
+            "facade_get_dependencies_ms": fm, "spans_per_s": cols.n_spans / (qm * 1e-3),
+            "note": "accept: host columns -> HBM + resident index merge; query: wall clock of select + gather + "
+                    "link + link() download, store resident in HBM; facade: InMemoryStorage.get_dependencies"
+                    "(endTs, lookback).execute() as shipped (insertion order, DependencyLink objects)",
+            "parity": "same links" if same and fsame else "MISMATCH"}
 
 
 def mysql_rows_leg(cols, S, device, max_spans=2_000_000, reps=3):
@@ -610,7 +636,14 @@ def main():
     ins_out = None
     side = world == 1 and config == "c2"  # the side legs run on C2 only
     if side and not args.no_insertion_order:
-        ictx = N.Context(S, device=local, insertion_order=True)
+        # the DependencyLinker facade's engine configuration: its table capacity for S services
+        # (_capacity: the dense LDS table up to 67) on an insertion-order context, service ranks set
+        from zipkin_amd.linker import _capacity
+        ictx = N.Context(_capacity(S), device=local, insertion_order=True)
+        names_w = synth.service_names(w)
+        rk = np.empty(S, np.int32)
+        rk[np.argsort(np.array(names_w, dtype=object), kind="stable")] = np.arange(S, dtype=np.int32)
+        ictx.set_ranks(N.ZDL_DICT_SERVICE, rk)
 
         def istep():
             ictx.reset()
@@ -626,7 +659,9 @@ def main():
         ictx.sync()
         it = (time.perf_counter() - t1) / ik
         ictx.close()
-        ins = {"ms_per_step": it * 1e3, "spans_per_s": cols.n_spans / it, "steps": ik, "parity": None}
+        ins = {"ms_per_step": it * 1e3, "spans_per_s": cols.n_spans / it, "steps": ik, "parity": None,
+               "capacity": _capacity(S), "note": "DependencyLinker facade's context: _capacity(S) services, "
+                                                 "insertion order, service ranks; link(ZDL_ORDER_INSERTION)"}
     # side measurement (not `value`): the same batch as a proto3 ListOfSpans decoded on the device
     # (zdl_decode_proto3) and linked from the decoded HBM columns
     p3 = None
@@ -642,8 +677,9 @@ def main():
             f"call {jleg['call_ms']:.1f} ms, links {jleg['parity']}")
     sleg = None
     if side and not args.no_store:
-        sleg = store_leg(cols, S, local, (p, c, n, e))
+        sleg = store_leg(cols, S, local, (p, c, n, e), synth.service_names(w))
         log(f"store getDependencies: {sleg['get_dependencies_ms']:.2f} ms (select {sleg['select_ms']:.2f} ms), "
+            f"facade {sleg['facade_get_dependencies_ms']:.2f} ms, accept {sleg['accept_ms']:.1f} ms, "
             f"links {sleg['parity']}")
     rows_leg = None
     if side and not args.no_mysql_rows:

@@ -95,6 +95,14 @@ extern "C" {
                                         and a multi-process job's RCCL reduce sums those tables); without
                                         it such a context keeps its links as one sorted list instead
                                         (a sparse context: no 16 * S^2 bytes of tables, S <= 46340) */
+#define ZDL_FLAG_TREE_STREAM 32u     /* every put records, per span, the tree the path that linked it
+                                        built - k_link's windows, k_mid, k_tail's big traces, the
+                                        giant tier, the exact paths - without sending anything to the
+                                        exact path: zdl_tree_export's node / parent, bfs = the traverse
+                                        index on an insertion-order context, 0 for a visited node on a
+                                        sorted one (-1 not visited), zdl_tree_reasons' ancestor =
+                                        firstRemoteAncestor's slot (parity tests of the benchmarked
+                                        kernels' trees; no time window) */
 #define ZDL_FLAG_TREE_EXPORT 8u      /* with ZDL_FLAG_INSERTION_ORDER: every put also records the tree
                                         SpanNode.Builder builds (SpanNode.java:122-249), read back by
                                         zdl_tree_export (parity tests of the tree itself, not only its
@@ -377,8 +385,8 @@ typedef struct zdl_decoded {
   uint64_t        n_spans;
   zdl_span_cols   dev;        /* device columns owned by the decoder (ord NULL), valid until
                                  the next decode; feed zdl_put_spans_device / zdl_store_append */
-  const uint64_t* trace_lo;   /* host copies (owned by the decoder) for the storage facade */
-  const int64_t*  timestamp;
+  const uint64_t* trace_lo;   /* NULL (ABI 3): nothing is copied to the host; zdl_decoder_download */
+  const int64_t*  timestamp;  /* copies the columns a caller needs */
   uint64_t        n_missing;  /* > 0: bind the keys, then zdl_decode_proto3_retry */
   const uint64_t* dev_trace_hi; /* device: each span's trace id high 64 bits (0 = 64-bit id), for
                                    zdl_store_append_traced */

@@ -37,25 +37,49 @@ def as_set(ls):
     return sorted((l.parent, l.child, l.call_count, l.error_count) for l in ls)
 
 
-@pytest.mark.parametrize("case", DL["cases"], ids=lambda c: c["name"])
-def test_golden_dependency_linker(case):
-    if case["mode"] == "log":  # asserts FINE log text only (the device's reason codes rendered)
-        from tests.test_gpu_finelog import _device_log
-        msgs, _ = _device_log([spans(t) for t in case["traces"]], name=case["name"])
-        assert all(m in msgs for m in case["log_contains"])
-        return
-    linker = DependencyLinker()
+# The engine paths the reference's vectors run through: the facade's default (insertion order,
+# k_link mode 4 + k_tail's exact path), the benchmarked streaming path (sorted output: k_link
+# mode 0 on the dense LDS table), and the table modes forced at the golden cases' small
+# dictionaries - LOG (ZDL_TM=log: k_link's emit log + k_scatter / k_hist), sorted and ranked,
+# and the sparse list (ZDL_SPARSE=1: TM_SORT + the log's sort/merge, sorted output only).
+PATHS = {"insertion": (True, {}), "sorted": (False, {}), "sorted_log": (False, {"ZDL_TM": "log"}),
+         "insertion_log": (True, {"ZDL_TM": "log"}), "sorted_sparse": (False, {"ZDL_SPARSE": "1"})}
+
+
+def _path(name, monkeypatch):
+    ins, env = PATHS[name]
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    return ins
+
+
+@pytest.mark.parametrize("case", [c for c in DL["cases"] if c["mode"] == "log"], ids=lambda c: c["name"])
+def test_golden_dependency_linker_log(case):
+    """The cases that assert FINE log text only: the device's reason codes rendered."""
+    from tests.test_gpu_finelog import _device_log
+    msgs, _ = _device_log([spans(t) for t in case["traces"]], name=case["name"])
+    assert all(m in msgs for m in case["log_contains"])
+
+
+@pytest.mark.parametrize("path", list(PATHS))
+@pytest.mark.parametrize("case", [c for c in DL["cases"] if c["mode"] != "log"], ids=lambda c: c["name"])
+def test_golden_dependency_linker(case, path, monkeypatch):
+    ins = _path(path, monkeypatch)
+    linker = DependencyLinker(insertion_order=ins)
     for t in case["traces"]:
         linker.put_trace(spans(t))
-    check_links(linker.link(), case["expect"], case["mode"])
+    # containsExactly needs the reference's list order: sorted paths are compared as sets
+    check_links(linker.link(), case["expect"], case["mode"] if ins else "only")
     linker.close()
 
 
+@pytest.mark.parametrize("path", ["insertion", "insertion_log"])
 @pytest.mark.parametrize("case", [c for c in DL["cases"] if c["mode"] == "exact"],
                          ids=lambda c: c["name"])
-def test_golden_response_bytes(case):
+def test_golden_response_bytes(case, path, monkeypatch):
     """The JSON_V1 bytes of the device's links equal those of the expected links, in order."""
     from zipkin_amd.codec import encode_links
+    _path(path, monkeypatch)
     linker = DependencyLinker()
     for t in case["traces"]:
         linker.put_trace(spans(t))
@@ -63,14 +87,32 @@ def test_golden_response_bytes(case):
     linker.close()
 
 
+@pytest.mark.parametrize("path", ["sorted", "sorted_log", "sorted_sparse"])
+@pytest.mark.parametrize("case", [c for c in DL["cases"] if c["mode"] != "log"], ids=lambda c: c["name"])
+def test_golden_response_bytes_sorted(case, path, monkeypatch):
+    """The sorted paths' JSON_V1 bytes equal the expected links' bytes in (parent, child) order."""
+    from zipkin_amd.codec import encode_links
+    _path(path, monkeypatch)
+    linker = DependencyLinker(insertion_order=False)
+    for t in case["traces"]:
+        linker.put_trace(spans(t))
+    got = linker.link()
+    linker.close()
+    if isinstance(case["expect"], dict):
+        return
+    exp = sorted(links(case["expect"]), key=lambda l: (l.parent, l.child))
+    assert encode_links(got) == encode_links(exp)
+
+
 @pytest.mark.parametrize("case", DL["merge_cases"], ids=lambda c: c["name"])
 def test_golden_merge_exact_order(case):
     check_links(DependencyLinker.merge(links(case["links"])), case["expect"], case["mode"])
 
 
+@pytest.mark.parametrize("path", list(PATHS))
 @pytest.mark.parametrize("case", ST["cases"], ids=lambda c: c["name"])
-def test_golden_storage(case):
-    store = InMemoryStorage(strict_trace_id=True)
+def test_golden_storage(case, path, monkeypatch):
+    store = InMemoryStorage(strict_trace_id=True, insertion_order=_path(path, monkeypatch))
     for b in case["batches"]:
         store.accept(spans(b)).execute()
     for q in case["queries"]:

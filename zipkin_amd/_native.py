@@ -24,6 +24,7 @@ ZDL_FLAG_TIMING = 1
 ZDL_FLAG_TIMING_ALL = 2
 ZDL_FLAG_INSERTION_ORDER = 4
 ZDL_FLAG_TREE_EXPORT = 8
+ZDL_FLAG_TREE_STREAM = 32
 ZDL_FLAG_DENSE_TABLE = 16
 ZDL_AKEY_NONE, ZDL_AKEY_LC, ZDL_AKEY_CA, ZDL_AKEY_CS, ZDL_AKEY_SA, ZDL_AKEY_SR, ZDL_AKEY_ERROR = range(7)
 
@@ -234,13 +235,14 @@ class Context:
 
     def __init__(self, n_services: int, device: int = 0, timing: bool = False, timing_all: bool = False,
                  timing_stride: int = 1, insertion_order: bool = False, device_ids=None,
-                 tree_export: bool = False, dense_table: bool = False):
+                 tree_export: bool = False, dense_table: bool = False, tree_stream: bool = False):
         """device_ids: a device group (zdl_config.device_ids): traces sharded over these GPUs,
         the tables summed by RCCL at link()."""
         L = lib()
         flags = (ZDL_FLAG_TIMING if timing else 0) | (ZDL_FLAG_TIMING_ALL if timing_all else 0)
         flags |= ZDL_FLAG_INSERTION_ORDER if insertion_order else 0
         flags |= ZDL_FLAG_TREE_EXPORT if tree_export else 0
+        flags |= ZDL_FLAG_TREE_STREAM if tree_stream else 0
         flags |= ZDL_FLAG_DENSE_TABLE if dense_table else 0
         ids = None
         if device_ids is not None:
@@ -562,14 +564,14 @@ class Decoder:
     def bind(self, dict_id: int, key: bytes, id_: int):
         self.check(self._L.zdl_decoder_bind(self.h, int(dict_id), bytes(key), len(key), int(id_)))
 
-    def download(self, n: int):
-        """The last decode's columns as host numpy arrays (dict by column name)."""
-        cols = dict(trace_lo=np.empty(n, np.uint64), id=np.empty(n, np.uint64), parent_id=np.empty(n, np.uint64),
-                    local_svc=np.empty(n, np.int32), remote_svc=np.empty(n, np.int32),
-                    local_ip4=np.empty(n, np.int32), local_ip6=np.empty(n, np.int32),
-                    port_flags=np.empty(n, np.uint32), timestamp=np.empty(n, np.int64))
-        sc = SpanCols(*(_ptr(cols[k]) for k in ("trace_lo", "id", "parent_id", "local_svc", "remote_svc",
-                                                 "local_ip4", "local_ip6", "port_flags", "timestamp")), None)
+    _COLS = (("trace_lo", np.uint64), ("id", np.uint64), ("parent_id", np.uint64), ("local_svc", np.int32),
+             ("remote_svc", np.int32), ("local_ip4", np.int32), ("local_ip6", np.int32), ("port_flags", np.uint32),
+             ("timestamp", np.int64))
+
+    def download(self, n: int, names=None):
+        """The last decode's columns (all, or `names`) as host numpy arrays (dict by column name)."""
+        cols = {k: np.empty(n, t) for k, t in self._COLS if names is None or k in names}
+        sc = SpanCols(*(_ptr(cols[k]) if k in cols else None for k, _ in self._COLS), None)
         self.check(self._L.zdl_decoder_download(self.h, C.byref(sc)))
         return cols
 

@@ -169,6 +169,8 @@ struct Args {
   // the device-wide big-trace tier (zdl_giant.inc): per back-list index, 1 = linked there,
   // 2 = k_tail's exact path, 0 = k_tail as usual; null when the tier did not run
   const uint8_t* gstat;
+  const uint32_t* grest;    // and then the back-list indexes k_tail links instead of the whole back
+  const uint32_t* grest_n;  // list (the giant ones dropped; the ones the tier rejected appended)
 };
 // The counter block of one put (two alternate by put, so no put issues a memset)
 enum : int { CTR_MID = 0, CTR_CX = 1, CTR_LARGE = 2, CTR_TICK_LARGE = 3, CTR_TICK_MID = 4, CTR_RETRY = 5, CTR_N = 8 };
@@ -469,6 +471,10 @@ __device__ __forceinline__ bool big_simple(const Args& A, unsigned char* lds, si
     v.a[i] = par;
     v.nm[i] = par;
     if (par >= 0) v.hasc[par] = 1;
+    if (A.tr_parent) {  // ZDL_FLAG_TREE_STREAM
+      A.tr_node[b + i] = (int32_t)(b + i);
+      A.tr_parent[b + i] = i == rp ? -2 : (par >= 0 ? (int32_t)(b + par) : -1);
+    }
   }
   __syncthreads();
   // 3. pointer jumping: a -> PAR_TERMINAL iff reachable, nm -> nearest ancestor with a kind
@@ -494,6 +500,12 @@ __device__ __forceinline__ bool big_simple(const Args& A, unsigned char* lds, si
     __syncthreads();
     if (!sh_more) break;
   }
+  if (A.tr_parent)
+    for (int i = threadIdx.x; i < n; i += BIG_WG) {
+      const bool rch = v.a[i] == PAR_TERMINAL;
+      A.tr_bfs[b + i] = rch ? 0 : -1;
+      A.tr_anc[b + i] = rch && v.nm[i] >= 0 ? (int32_t)(b + v.nm[i]) : -1;
+    }
   // 4. DependencyLinker's rules per node (every span of a simple trace is a node)
   for (int i = threadIdx.x; i < n; i += BIG_WG) {
     if (v.a[i] != PAR_TERMINAL) continue;  // unreachable (a cycle not through the root)
@@ -727,6 +739,10 @@ __device__ __forceinline__ bool wave_big(const Args& A, unsigned char* p, uint32
     v.a[i] = (int16_t)par;
     v.nm[i] = (int16_t)par;
     if (par >= 0) v.hasc[par] = 1;
+    if (A.tr_parent) {  // ZDL_FLAG_TREE_STREAM
+      A.tr_node[b + i] = (int32_t)(b + i);
+      A.tr_parent[b + i] = i == rp ? -2 : (par >= 0 ? (int32_t)(b + par) : -1);
+    }
   }
   wave_sync();
   // 3. pointer jumping: a -> PAR_TERMINAL iff reachable, nm -> nearest ancestor with a kind
@@ -751,6 +767,16 @@ __device__ __forceinline__ bool wave_big(const Args& A, unsigned char* p, uint32
     }
     wave_sync();
     if (!ballot(more)) break;
+  }
+  if (A.tr_parent) {
+#pragma unroll
+    for (int k = 0; k < WB_K; ++k) {
+      const int i = lane + 64 * k;
+      if (i >= n) continue;
+      const bool rch = v.a[i] == PAR_TERMINAL;
+      A.tr_bfs[b + i] = rch ? 0 : -1;
+      A.tr_anc[b + i] = rch && v.nm[i] >= 0 ? (int32_t)(b + v.nm[i]) : -1;
+    }
   }
   // 4. DependencyLinker's rules per node (DependencyLinker.java:58-148)
   auto emit = [&](int32_t x, int32_t y, bool er) {
@@ -933,7 +959,7 @@ __device__ __forceinline__ void big_exact(const Args& A, uint64_t b, int n, uint
     big_bfs(v, n, rp, A.o_key + b, A.o_fa + b, A.o_fb + b, bfs);
     big_sync();
   }
-  if (ORD && A.tr_parent) {  // ZDL_FLAG_TREE_EXPORT (wave_tree_export's encoding)
+  if (A.tr_parent) {  // ZDL_FLAG_TREE_EXPORT / _STREAM (wave_tree_export's encoding)
     for (int p = threadIdx.x; p < n; p += BIG_WG) {
       int head = p;
       while (!v.live[head] && head > 0 && v.id[v.perm[head - 1]] == v.id[v.perm[p]]) --head;
@@ -945,7 +971,7 @@ __device__ __forceinline__ void big_exact(const Args& A, uint64_t b, int n, uint
         pr = p == rp ? -2 : (par == PAR_TERMINAL ? -1 : (int32_t)(b + v.perm[par]));
         int q = par, steps = 0;
         while (q >= 0 && steps++ <= n) q = v.parent[q];
-        if (q == PAR_TERMINAL) bf = (int32_t)bfs[p];
+        if (q == PAR_TERMINAL) bf = ORD ? (int32_t)bfs[p] : 0;
       }
       A.tr_parent[slot] = pr;
       A.tr_bfs[slot] = bf;
@@ -1200,7 +1226,7 @@ __global__ void __launch_bounds__(TAIL_WG, 1) k_tail(Args A) {
   // simple), one workgroup each, by ticket (the next one fetched while this trace is linked),
   // so that a giant trace delays only its own workgroup
   __shared__ uint32_t sh_j;
-  const uint32_t nlarge = *A.large_count;
+  const uint32_t nlarge = A.grest ? *A.grest_n : *A.large_count;
   const uint32_t nbig = nlarge + (A.wb_max ? *A.retry_count : 0u);
   if (nbig) {
     if (threadIdx.x == 0) sh_j = atomicAdd(A.tick_large, 1u);
@@ -1211,7 +1237,7 @@ __global__ void __launch_bounds__(TAIL_WG, 1) k_tail(Args A) {
       if (j >= nbig) break;
       if (threadIdx.x == 0) sh_j = atomicAdd(A.tick_large, 1u);
       const bool back = j < nlarge;
-      const uint32_t bi = back ? A.big_cap - 1u - j : A.retry[j - nlarge];
+      const uint32_t bi = back ? (A.grest ? A.grest[j] : A.big_cap - 1u - j) : A.retry[j - nlarge];
       const uint8_t gs = back && A.gstat ? A.gstat[bi] : 0;  // the giant tier's verdict (uniform)
       if (gs != 1) big_one<ORD>(A, lds, tail_block_bytes(WINDOW), bi, back && gs == 0);
     }
@@ -1404,7 +1430,9 @@ struct zdl_ctx {
   DevBuf<uint32_t> b_hv;
   // the device-wide big-trace tier (zdl_giant.inc, sparse contexts): per-put lists and scratch
   int giant_min = 2048;  // traces longer than this (ZDL_GIANT_MIN; 0: off, k_tail's workgroups)
-  DevBuf<uint32_t> gg_bi, gg_n, gg_tile0, gg_bad, gg_tile_g, gg_bstart, gg_blen, gg_meta, gg_H;
+  DevBuf<uint32_t> gg_bi, gg_n, gg_tile0, gg_bad, gg_tile_g, gg_bstart, gg_blen, gg_meta, gg_H, gg_rest;
+  DevBuf<unsigned long long> gg_sc0, gg_sc1;
+  DevBuf<unsigned char> gg_tmp;
   DevBuf<uint64_t> gg_base, gg_h0;
   DevBuf<unsigned long long> gg_root, gg_tsroot, gg_tsmin;
   DevBuf<int32_t> gg_rootidx;
@@ -1593,6 +1621,11 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
     c->sparse = want && cfg->n_services <= 46340u &&
                 !(cfg->flags & (ZDL_FLAG_INSERTION_ORDER | ZDL_FLAG_DENSE_TABLE));
   }
+  if ((cfg->flags & ZDL_FLAG_TREE_EXPORT) && (cfg->flags & ZDL_FLAG_TREE_STREAM)) {
+    delete c;
+    g_create_error = "ZDL_FLAG_TREE_EXPORT and ZDL_FLAG_TREE_STREAM exclude each other";
+    return nullptr;
+  }
   if ((cfg->flags & ZDL_FLAG_TREE_EXPORT) && !c->ord) {
     delete c;
     g_create_error = "ZDL_FLAG_TREE_EXPORT needs ZDL_FLAG_INSERTION_ORDER (the exact per-trace path)";
@@ -1629,8 +1662,8 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
     for (int tm = 0; tm < 3 && e == hipSuccess; ++tm)
       e = hipFuncSetAttribute(k_link_fn(tm, w), hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)link_block_bytes(w, tm));
-    for (int m = 1; m <= 4 && e == hipSuccess; ++m)
-      for (int tm = 0; tm < (m == 4 ? 3 : 2) && e == hipSuccess; ++tm)
+    for (int m = 1; m <= 5 && e == hipSuccess; ++m)
+      for (int tm = 0; tm < (m == 5 ? 4 : m == 4 ? 3 : 2) && e == hipSuccess; ++tm)
         e = hipFuncSetAttribute(k_link_fn(tm, w, m), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)link_block_bytes(m == 3 ? 0 : w, tm, m));
   }
@@ -1644,9 +1677,10 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
   if (e == hipSuccess) {
     const char* pe = getenv("ZDL_PROF");
     c->prof_on = pe && pe[0] == '1';
-    if (c->prof_on) {
-      e = c->prof.ensure(12);
-      if (e == hipSuccess) e = hipMemsetAsync(c->prof.p, 0, 12 * 8, c->stream);
+    if (c->prof_on) {  // 12 phase counters, then (start, end) wall clock of every k_link wave
+      const size_t words = 12 + 2 * (size_t)c->cus * lk::wgs_per_cu * lk::waves(0);
+      e = c->prof.ensure(words);
+      if (e == hipSuccess) e = hipMemsetAsync(c->prof.p, 0, words * 8, c->stream);
     }
     const char* sk = getenv("ZDL_SKIP");
     c->skip = sk ? (uint32_t)strtoul(sk, nullptr, 0) : 0u;
@@ -1700,6 +1734,29 @@ void zdl_destroy(zdl_ctx* c) {
       for (int k = 0; k < 12; ++k) fprintf(stderr, " %d:%.1f%%", k, tot > 0 ? 100.0 * (double)h[k] / tot : 0.0);
       fprintf(stderr, " total %.3e\n", tot);
     }
+    // the last put's k_link waves: when each finished after the first one started (100 MHz clock)
+    const size_t W = (size_t)c->cus * lk::wgs_per_cu * lk::waves(0);
+    std::vector<unsigned long long> w(2 * W);
+    if (hipMemcpy(w.data(), c->prof.p + 12, 2 * W * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+      unsigned long long t0 = ~0ull;
+      for (size_t i = 0; i < W; ++i)
+        if (w[2 * i]) t0 = std::min(t0, w[2 * i]);
+      std::vector<double> end, busy;
+      for (size_t i = 0; i < W; ++i)
+        if (w[2 * i] && w[2 * i + 1]) {
+          end.push_back((double)(w[2 * i + 1] - t0) * 0.01);
+          busy.push_back((double)(w[2 * i + 1] - w[2 * i]) * 0.01);
+        }
+      std::sort(end.begin(), end.end());
+      std::sort(busy.begin(), busy.end());
+      if (!end.empty()) {
+        auto q = [&](const std::vector<double>& v, double f) { return v[std::min(v.size() - 1, (size_t)(f * v.size()))]; };
+        fprintf(stderr, "[zdl prof] k_link waves %zu: end us min %.1f p10 %.1f p50 %.1f p90 %.1f p99 %.1f max %.1f; "
+                        "busy us p10 %.1f p50 %.1f p90 %.1f max %.1f\n",
+                end.size(), end.front(), q(end, 0.1), q(end, 0.5), q(end, 0.9), q(end, 0.99), end.back(), q(busy, 0.1),
+                q(busy, 0.5), q(busy, 0.9), busy.back());
+      }
+    }
   }
   c->prof.release();
   c->lg.release(); c->lg_grp.release(); c->lg_n.release(); c->lg_cnt.release(); c->lg_tot.release();
@@ -1713,8 +1770,9 @@ void zdl_destroy(zdl_ctx* c) {
   c->b_ip6.release(); c->b_parent.release(); c->b_pf.release(); c->b_perm.release(); c->b_live.release();
   c->b_hasc.release(); c->b_nm.release(); c->b_hk.release(); c->b_hv.release();
   for (auto* b : {&c->gg_bi, &c->gg_n, &c->gg_tile0, &c->gg_bad, &c->gg_tile_g, &c->gg_bstart, &c->gg_blen,
-                  &c->gg_meta, &c->gg_H})
+                  &c->gg_meta, &c->gg_H, &c->gg_rest})
     b->release();
+  c->gg_sc0.release(); c->gg_sc1.release(); c->gg_tmp.release();
   c->gg_base.release(); c->gg_h0.release(); c->gg_root.release(); c->gg_tsroot.release(); c->gg_tsmin.release();
   c->gg_rootidx.release(); c->gg_stat.release();
   if (c->h_gmeta) (void)hipHostFree(c->h_gmeta);
@@ -1939,6 +1997,9 @@ static int giant_run(zdl_ctx* c, Args& A, uint64_t n_spans, uint64_t n_traces) {
   HIP_TRY(c, c->gg_bstart.ensure(ntmax));
   HIP_TRY(c, c->gg_blen.ensure(ntmax));
   HIP_TRY(c, c->gg_meta.ensure(GM_WORDS));
+  HIP_TRY(c, c->gg_rest.ensure(nl));
+  HIP_TRY(c, c->gg_sc0.ensure(nl));
+  HIP_TRY(c, c->gg_sc1.ensure(nl));
   GArgs G{};
   G.bi = c->gg_bi.p;
   G.base = c->gg_base.p;
@@ -1956,13 +2017,31 @@ static int giant_run(zdl_ctx* c, Args& A, uint64_t n_spans, uint64_t n_traces) {
   G.meta = c->gg_meta.p;
   G.gstat = c->gg_stat.p;
   G.gmin = (uint32_t)c->giant_min;
-  hipLaunchKernelGGL(k_g_prep, dim3(1), dim3(BIG_WG), 0, s, A, G);
+  G.rest = c->gg_rest.p;
+  G.sc0 = c->gg_sc0.p;
+  G.sc1 = c->gg_sc1.p;
+  G.nl = nl;
+  // the giant traces of the back list placed by two scans (tiles | counts, matrix sizes)
+  HIP_TRY(c, hipMemsetAsync(c->gg_meta.p, 0, GM_WORDS * 4, s));
+  hipLaunchKernelGGL(k_g_mark, dim3((nl + 255) / 256), dim3(256), 0, s, A, G);
+  HIP_TRY(c, hipGetLastError());
+  size_t need = 0, need1 = 0;
+  HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(nullptr, need, c->gg_sc0.p, c->gg_sc0.p, (int)nl, s));
+  HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(nullptr, need1, c->gg_sc1.p, c->gg_sc1.p, (int)nl, s));
+  HIP_TRY(c, c->gg_tmp.ensure(std::max(need, need1)));
+  need = c->gg_tmp.n;
+  HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(c->gg_tmp.p, need, c->gg_sc0.p, c->gg_sc0.p, (int)nl, s));
+  need = c->gg_tmp.n;
+  HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(c->gg_tmp.p, need, c->gg_sc1.p, c->gg_sc1.p, (int)nl, s));
+  hipLaunchKernelGGL(k_g_write, dim3((nl + 255) / 256), dim3(256), 0, s, A, G);
   HIP_TRY(c, hipGetLastError());
   HIP_TRY(c, hipMemcpyAsync(c->h_gmeta, c->gg_meta.p, GM_WORDS * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(c, hipStreamSynchronize(s));
   const uint32_t ng = c->h_gmeta[GM_G], nt = c->h_gmeta[GM_NT], maxn = c->h_gmeta[GM_MAXN], nh = c->h_gmeta[GM_NH];
-  A.gstat = c->gg_stat.p;  // every back-list entry has its verdict now (0 when no giant)
-  if (ng == 0) return ZDL_OK;
+  if (ng == 0) return ZDL_OK;  // k_tail takes the whole back list as usual
+  A.gstat = c->gg_stat.p;  // every back-list entry has its verdict now
+  A.grest = c->gg_rest.p;  // k_tail links the rest list only (k_g_par appends rejected giants)
+  A.grest_n = c->gg_meta.p + GM_REST;
   if (nt > ntmax || maxn > (uint32_t)GMAXN) return fail(c, ZDL_EDEVICE, "giant tier: inconsistent sizes");
   HIP_TRY(c, c->gg_H.ensure(nh));
   G.H = c->gg_H.p;
@@ -1974,9 +2053,12 @@ static int giant_run(zdl_ctx* c, Args& A, uint64_t n_spans, uint64_t n_traces) {
   hipLaunchKernelGGL(k_g_scatter, tg, tb, 0, s, A, G);
   hipLaunchKernelGGL(k_g_join, tg, tb, GHCAP * 16, s, A, G);
   hipLaunchKernelGGL(k_g_par, tg, tb, 0, s, A, G);
-  int rounds = 2;  // after r rounds a points 2^r generations up: enough once 2^r >= the depth
-  while (rounds < GROUNDS_MAX && (1u << (rounds - 1)) < maxn) ++rounds;
-  for (int r = 0; r < rounds; ++r) hipLaunchKernelGGL(k_g_jump, tg, tb, 0, s, A, G, r);
+  // after r rounds of two hops a points at least 3^r generations up: enough once 3^r >= the
+  // depth (<= n); rounds after convergence return at once (the flag)
+  int rounds = 1;
+  for (uint64_t reach = 3; reach < (uint64_t)maxn && rounds < GROUNDS_MAX; reach *= 3) ++rounds;
+  const dim3 jg(std::min<uint32_t>(8 * G.per, (uint32_t)c->cus * 2));  // persistent; a multiple of 8
+  for (int r = 0; r < rounds; ++r) hipLaunchKernelGGL(k_g_jump, jg, tb, 0, s, A, G, r);
   hipLaunchKernelGGL(k_g_rules, tg, tb, 0, s, A, G);
   HIP_TRY(c, hipGetLastError());
   return ZDL_OK;
@@ -2044,7 +2126,7 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   A.cx_win = c->cx_win.p;
   A.skip = c->skip;
   A.prof = c->prof.p;
-  const int lmode = plan_only ? 3 : c->ord ? 4 : (c->prof_on ? 1 : (c->skip ? 2 : 0));
+  const int lmode = plan_only ? 3 : c->ord ? 4 : (c->flags & ZDL_FLAG_TREE_STREAM) ? 5 : (c->prof_on ? 1 : (c->skip ? 2 : 0));
   const uint32_t lW = (uint32_t)lgrid * (uint32_t)lk::waves(c->window, lmode);  // k_link's waves
   const uint32_t lP = (uint32_t)((SS + (1u << PSHIFT) - 1) >> PSHIFT);
   if (tm == TM_SORT) {  // k_link's segments in [0, 2n), k_tail's in [2n, 4n)
@@ -2112,7 +2194,9 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
     HIP_TRY(c, c->retry.ensure(n_traces));
     A.retry = c->retry.p;
   }
-  if (c->flags & ZDL_FLAG_TREE_EXPORT) {  // the last put's tree (insertion-order contexts only)
+  if (c->flags & (ZDL_FLAG_TREE_EXPORT | ZDL_FLAG_TREE_STREAM)) {  // the last put's tree
+    if ((c->flags & ZDL_FLAG_TREE_STREAM) && c->window)
+      return fail(c, ZDL_EINVAL, "ZDL_FLAG_TREE_STREAM: no time window");
     HIP_TRY(c, c->tr_node.ensure(n_spans));
     HIP_TRY(c, c->tr_parent.ensure(n_spans));
     HIP_TRY(c, c->tr_bfs.ensure(n_spans));
@@ -2359,6 +2443,7 @@ hipError_t store_compact_dev(zdl_store* st, const uint32_t* idx, uint64_t n_keep
   st->n = n_keep;
   st->cap = cap;
   st->sel_valid = false;
+  st->iw.ni = 0;  // positions renumbered: the resident index is rebuilt by the next update
   return hipSuccess;
 }
 
@@ -2431,6 +2516,7 @@ int zdl_store_clear(zdl_store* st) {
   if (!st) return ZDL_EINVAL;
   st->n = st->n_alive = 0;
   st->sel_valid = false;
+  st->iw.ni = 0;
   return ZDL_OK;
 }
 
@@ -2477,6 +2563,9 @@ int zdl_store_append_traced(zdl_store* st, const zdl_span_cols* col, const uint6
     e = col->timestamp ? hipMemcpyAsync(st->ts.p + o, col->timestamp, n * 8, hipMemcpyDefault, s)
                        : hipMemsetAsync(st->ts.p + o, 0, n * 8, s);
   if (e == hipSuccess) e = hipMemsetAsync(st->alive.p + o, 1, n, s);
+  // the resident trace index takes the batch in (sorted, merged: the TreeMap inserts of
+  // InMemoryStorage.accept, IMS:156-181), so a query only filters and orders traces
+  if (e == hipSuccess) e = zdl::index_update(st->iw, st->lo.p, st->ts.p, st->n + n, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);  // the columns are borrowed for the call only
   if (e != hipSuccess) return store_hip_fail(st, e, "zdl_store_append");
   st->n += n;
@@ -2534,7 +2623,8 @@ int zdl_store_evict(zdl_store* st, uint64_t to_recover, uint64_t* evicted) {
   uint64_t ev = 0;
   bool exhausted = false;
   if (e == hipSuccess)
-    e = zdl::index_evict(st->iw, st->lo.p, st->ts.p, st->alive.p, st->n, to_recover, &ev, &exhausted, st->stream);
+    e = zdl::index_evict(st->iw, st->lo.p, st->ts.p, st->alive.p, st->n, st->n_alive, to_recover, &ev, &exhausted,
+                         st->stream);
   if (e != hipSuccess) return store_hip_fail(st, e, "zdl_store_evict");
   st->n_alive -= ev;
   st->sel_valid = false;
@@ -2555,7 +2645,8 @@ int zdl_store_select(zdl_store* st, int mode, uint64_t* n_sel, uint64_t* n_trace
   if (e == hipSuccess) e = st->sel_off.ensure(st->n + 1);
   const int m = mode == ZDL_SELECT_NEWEST ? zdl::SEL_NEWEST : mode == ZDL_SELECT_ALL ? zdl::SEL_ALL : zdl::SEL_ALL_STRICT;
   if (e == hipSuccess)
-    e = zdl::index_select(st->iw, st->lo.p, st->hi.p, st->ts.p, st->alive.p, st->n, m, st->sel.p, st->sel_off.p,
+    e = zdl::index_select(st->iw, st->lo.p, st->hi.p, st->ts.p, st->alive.p, st->n, st->n_alive, m, st->sel.p,
+                          st->sel_off.p,
                           &st->sel_n, &st->sel_traces, st->stream);
   if (e != hipSuccess) return store_hip_fail(st, e, "zdl_store_select");
   st->sel_valid = true;
@@ -3564,7 +3655,8 @@ extern "C" {
 
 int zdl_tree_export(zdl_ctx* c, int32_t* node_of, int32_t* parent, int32_t* bfs, uint64_t n) {
   if (!c || !node_of || !parent || !bfs) return ZDL_EINVAL;
-  if (!(c->flags & ZDL_FLAG_TREE_EXPORT) || !c->sub.empty()) return fail(c, ZDL_EINVAL, "context without ZDL_FLAG_TREE_EXPORT");
+  if (!(c->flags & (ZDL_FLAG_TREE_EXPORT | ZDL_FLAG_TREE_STREAM)) || !c->sub.empty())
+    return fail(c, ZDL_EINVAL, "context without ZDL_FLAG_TREE_EXPORT / ZDL_FLAG_TREE_STREAM");
   if (n != c->tr_n) return fail(c, ZDL_EINVAL, "zdl_tree_export: n must be the last put's span count");
   const int rc = zdl_sync(c);
   if (rc != ZDL_OK) return rc;
@@ -3577,7 +3669,8 @@ int zdl_tree_export(zdl_ctx* c, int32_t* node_of, int32_t* parent, int32_t* bfs,
 
 int zdl_tree_reasons(zdl_ctx* c, uint8_t* reason, int32_t* ancestor, int32_t* link, int32_t* sorted, uint64_t n) {
   if (!c || !reason || !ancestor || !link || !sorted) return ZDL_EINVAL;
-  if (!(c->flags & ZDL_FLAG_TREE_EXPORT) || !c->sub.empty()) return fail(c, ZDL_EINVAL, "context without ZDL_FLAG_TREE_EXPORT");
+  if (!(c->flags & (ZDL_FLAG_TREE_EXPORT | ZDL_FLAG_TREE_STREAM)) || !c->sub.empty())
+    return fail(c, ZDL_EINVAL, "context without ZDL_FLAG_TREE_EXPORT / ZDL_FLAG_TREE_STREAM");
   if (n != c->tr_n) return fail(c, ZDL_EINVAL, "zdl_tree_reasons: n must be the last put's span count");
   const int rc = zdl_sync(c);
   if (rc != ZDL_OK) return rc;

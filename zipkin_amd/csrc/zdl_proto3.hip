@@ -555,8 +555,6 @@ struct zdl_decoder {
   DBuf<uint32_t> miss_len;
   DBuf<unsigned long long> status;  // [0] first_err, [1] any_miss (u32 in the low half)
   HBuf<unsigned long long> status_h;
-  HBuf<uint64_t> lo_h;
-  HBuf<int64_t> ts_h;
   std::vector<std::string> missing;  // kind byte + key bytes, first-seen order
   hipEvent_t ev[2] = {nullptr, nullptr};  // around the last k_proto3_spans / k_js_spans
   float kernel_ms = 0.f;
@@ -692,17 +690,11 @@ int run_kernel(zdl_decoder* d, zdl_decoded* out) {
     return ZDL_OK;
   }
   out->n_spans = n;
-  if (n) {
-    DEC_TRY(d, d->lo_h.ensure(n));
-    DEC_TRY(d, d->ts_h.ensure(n));
-    DEC_TRY(d, hipMemcpyAsync(d->lo_h.p, d->lo.p, n * 8, hipMemcpyDeviceToHost, s));
-    DEC_TRY(d, hipMemcpyAsync(d->ts_h.p, d->ts.p, n * 8, hipMemcpyDeviceToHost, s));
-    DEC_TRY(d, hipStreamSynchronize(s));
-  }
+  // device columns only: nothing crosses PCIe (zdl_decoder_download copies what a caller needs)
   out->dev = zdl_span_cols{d->lo.p, d->id.p, d->pid.p, d->lsvc.p, d->rsvc.p, d->ip4.p, d->ip6.p, d->pf.p, d->ts.p, nullptr};
-  out->trace_lo = d->lo_h.p;
+  out->trace_lo = nullptr;
   out->dev_trace_hi = d->hi.p;
-  out->timestamp = d->ts_h.p;
+  out->timestamp = nullptr;
   return ZDL_OK;
 }
 

@@ -1,8 +1,10 @@
 // zdl_store.hip — InMemoryStorage's trace index on the device (zdl_store_index.h).
 //
-// All passes are HBM-bound gathers, flag/scan kernels and stable LSD radix sorts (hipCUB) over
-// the alive spans: a getDependencies selection is four 64-bit (key, u32 position) sorts plus a
-// sort of one key per trace, an eviction one span sort and one trace sort. Counts (alive spans,
+// All passes are HBM-bound gathers, flag/scan kernels, stable LSD radix sorts and merges
+// (hipCUB). accept keeps the resident index current: the batch is sorted twice by (low id,
+// timestamp, arrival) and (low id, first arrival of its key, arrival) and merged into the two
+// resident orders. A getDependencies selection then filters the alive spans of the resident
+// order and sorts one key per trace; an eviction sorts one key per trace. Counts (alive spans,
 // traces, the eviction result) are the only values that come back to the host.
 #include "zdl_store_index.h"
 
@@ -62,6 +64,49 @@ __global__ void k_iota32(uint32_t* __restrict__ out, uint64_t m) {
   if (i < m) out[i] = (uint32_t)i;
 }
 
+__global__ void k_iota_from(uint32_t* __restrict__ out, uint64_t base, uint64_t m) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < m) out[i] = (uint32_t)(base + i);
+}
+
+// key[i] = src[idx[i]] (32-bit)
+__global__ void k_take32(const uint32_t* __restrict__ src, const uint32_t* __restrict__ idx, uint32_t* __restrict__ key,
+                         uint64_t m) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < m) key[i] = src[idx[i]];
+}
+
+// fs[bk[i]] = bk[head[i]]: a span's first arrival among the spans of its (low id, timestamp) key
+__global__ void k_first_arrival(const uint32_t* __restrict__ bk, const uint32_t* __restrict__ head, uint64_t m,
+                                uint32_t* __restrict__ fs) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < m) fs[bk[i]] = bk[head[i]];
+}
+
+// the resident orders' comparators (positions compared through the columns; the position last)
+struct LoTsLess {
+  const uint64_t* lo;
+  const int64_t* ts;
+  __device__ bool operator()(uint32_t a, uint32_t b) const {
+    if (lo[a] != lo[b]) return lo[a] < lo[b];
+    if (ts[a] != ts[b]) return ts[a] < ts[b];
+    return a < b;
+  }
+};
+struct LoFsLess {
+  const uint64_t* lo;
+  const uint32_t* fs;
+  __device__ bool operator()(uint32_t a, uint32_t b) const {
+    if (lo[a] != lo[b]) return lo[a] < lo[b];
+    if (fs[a] != fs[b]) return fs[a] < fs[b];
+    return a < b;
+  }
+};
+struct AliveOf {
+  const uint8_t* alive;
+  __device__ bool operator()(uint32_t p) const { return alive[p] != 0; }
+};
+
 // flag[i] = a new run of equal keys starts at i (keys sorted)
 __global__ void k_runs(const uint64_t* __restrict__ key, uint64_t m, uint8_t* __restrict__ flag) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -104,12 +149,6 @@ __global__ void k_key_heads(const uint64_t* __restrict__ lo, const int64_t* __re
   out[i] = h ? (uint32_t)i : 0u;
 }
 
-// storage-order key: (first arrival of the span's (lowTraceId, timestamp) key, arrival)
-__global__ void k_first_seen(const uint32_t* __restrict__ v, const uint32_t* __restrict__ head,
-                             uint64_t m, uint64_t* __restrict__ key) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < m) key[i] = ((uint64_t)v[head[i]] << 32) | v[i];
-}
 
 // segment j's newest timestamp (the last span of j in v, sorted by timestamp inside a low id),
 // as a descending key; segments fed in reverse (descending low id) so a stable sort breaks
@@ -306,6 +345,11 @@ void IndexWork::release() {
   if (tmp) (void)hipFree(tmp);
   if (d) (void)hipFree(d);
   if (h) (void)hipHostFree(h);
+  for (auto* p : {bk, st, fs, mo})
+    if (p) (void)hipFree(p);
+  bk = st = fs = mo = nullptr;
+  rcap = 0;
+  ni = 0;
   seg = nullptr;
   flag = nullptr;
   tmp = nullptr;
@@ -328,30 +372,111 @@ hipError_t index_alive(IndexWork& w, const uint8_t* alive, uint64_t n, uint32_t*
   return hipSuccess;
 }
 
+namespace {
+// grows the resident arrays keeping positions [0, ni)
+hipError_t reserve_resident(IndexWork& w, uint64_t n, hipStream_t s) {
+  if (n <= w.rcap) return hipSuccess;
+  const size_t cap = std::max<size_t>(n + n / 2, 1 << 16);
+  uint32_t* nb[4] = {};
+  for (auto*& p : nb) ITRY(hipMalloc((void**)&p, cap * sizeof(uint32_t)));
+  if (w.ni) {
+    ITRY(hipMemcpyAsync(nb[0], w.bk, w.ni * 4, hipMemcpyDeviceToDevice, s));
+    ITRY(hipMemcpyAsync(nb[1], w.st, w.ni * 4, hipMemcpyDeviceToDevice, s));
+    ITRY(hipMemcpyAsync(nb[2], w.fs, w.ni * 4, hipMemcpyDeviceToDevice, s));
+    ITRY(hipStreamSynchronize(s));
+  }
+  for (auto* p : {w.bk, w.st, w.fs, w.mo})
+    if (p) (void)hipFree(p);
+  w.bk = nb[0];
+  w.st = nb[1];
+  w.fs = nb[2];
+  w.mo = nb[3];
+  w.rcap = cap;
+  return hipSuccess;
+}
+
+template <class Cmp>
+hipError_t merge_into(IndexWork& w, uint32_t*& res, const uint32_t* batch, uint64_t n0, uint64_t b, Cmp cmp,
+                      hipStream_t s) {
+  if (n0 == 0) {
+    ITRY(hipMemcpyAsync(res, batch, b * 4, hipMemcpyDeviceToDevice, s));
+    return step_done(s, __LINE__);
+  }
+  ITRY(cub_at(w, s, __LINE__, [&](void* t, size_t& bytes) {
+    return hipcub::DeviceMerge::MergeKeys(t, bytes, res, (int)n0, batch, (int)b, w.mo, cmp, s);
+  }));
+  std::swap(res, w.mo);
+  return hipSuccess;
+}
+
+// the alive positions of a resident order (stable): into out, their number into *m (a sync);
+// every position when nothing is evicted
+hipError_t alive_of(IndexWork& w, const uint32_t* order, const uint8_t* alive, uint64_t n, uint64_t n_alive,
+                    uint32_t* out, uint64_t* m, hipStream_t s) {
+  if (n_alive == n) {
+    ITRY(hipMemcpyAsync(out, order, n * 4, hipMemcpyDeviceToDevice, s));
+    *m = n;
+    return step_done(s, __LINE__);
+  }
+  ITRY(cub_at(w, s, __LINE__, [&](void* t, size_t& b) {
+    return hipcub::DeviceSelect::If(t, b, order, out, w.d, (int)n, AliveOf{alive}, s);
+  }));
+  ITRY(fetch(w, 1, s));
+  *m = w.h[0];
+  return hipSuccess;
+}
+}  // namespace
+
+hipError_t index_update(IndexWork& w, const uint64_t* lo, const int64_t* ts, uint64_t n, hipStream_t s) {
+  if (n >= (1ull << 31)) return hipErrorInvalidValue;
+  if (w.ni > n) w.ni = 0;  // renumbered (compaction) or cleared: rebuild
+  if (w.ni == n) return hipSuccess;
+  ITRY(reserve(w, n));  // before any w buffer is named: reserve reallocates them
+  ITRY(reserve_resident(w, n, s));
+  const uint64_t n0 = w.ni, b = n - n0;
+  const uint64_t* ts64 = reinterpret_cast<const uint64_t*>(ts);
+  // the batch by (low id, timestamp, arrival): stable sorts by timestamp, then by low id
+  LAUNCH(k_iota_from, b, w.v[0], n0, b);
+  LAUNCH(k_take, b, ts64, w.v[0], kSign, w.k[0], b);
+  ITRY(sort64(w, w.k[0], w.k[1], w.v[0], w.v[1], b, s));
+  LAUNCH(k_take, b, lo, w.v[1], 0ull, w.k[0], b);
+  ITRY(sort64(w, w.k[0], w.k[1], w.v[1], w.v[0], b, s));
+  ITRY(merge_into(w, w.bk, w.v[0], n0, b, LoTsLess{lo, ts}, s));
+  // every span's first arrival among its (low id, timestamp) key (the old ones' do not change:
+  // a new span arrives after every indexed one)
+  LAUNCH(k_key_heads, n, lo, ts, w.bk, n, w.u[0]);
+  ITRY(max_scan(w, w.u[0], w.u[1], n, s));
+  LAUNCH(k_first_arrival, n, w.bk, w.u[1], n, w.fs);
+  // the batch by (low id, first arrival, arrival)
+  LAUNCH(k_iota_from, b, w.v[0], n0, b);
+  LAUNCH(k_take32, b, w.fs, w.v[0], w.u[2], b);
+  ITRY(sort32(w, w.u[2], w.u[3], w.v[0], w.v[1], b, s));
+  LAUNCH(k_take, b, lo, w.v[1], 0ull, w.k[0], b);
+  ITRY(sort64(w, w.k[0], w.k[1], w.v[1], w.v[0], b, s));
+  ITRY(merge_into(w, w.st, w.v[0], n0, b, LoFsLess{lo, w.fs}, s));
+  w.ni = n;
+  return hipSuccess;
+}
+
 hipError_t index_select(IndexWork& w, const uint64_t* lo, const uint64_t* hi, const int64_t* ts,
-                        const uint8_t* alive, uint64_t n, int mode, uint32_t* perm, uint64_t* off,
-                        uint64_t* n_sel, uint64_t* n_traces, hipStream_t s) {
+                        const uint8_t* alive, uint64_t n, uint64_t n_alive, int mode, uint32_t* perm,
+                        uint64_t* off, uint64_t* n_sel, uint64_t* n_traces, hipStream_t s) {
   uint64_t m = 0;
   *n_sel = *n_traces = 0;
   if (n >= (1ull << 31)) return hipErrorInvalidValue;
+  ITRY(index_update(w, lo, ts, n, s));  // accept keeps it current: normally nothing to do
   ITRY(reserve(w, n));  // before any w buffer is named: reserve reallocates them
-  ITRY(index_alive(w, alive, n, w.v[0], &m, s));
+  if (n == 0 || n_alive == 0) return hipSuccess;
+  uint32_t* const stored = w.v[1];  // low ids ascending, storage order inside (IMS:448-454)
+  uint32_t* const by_key = w.u[3];  // (low id, timestamp, arrival): the newest timestamps below
+  ITRY(alive_of(w, w.st, alive, n, n_alive, stored, &m, s));
   if (m == 0) return hipSuccess;
-  const uint64_t* ts64 = reinterpret_cast<const uint64_t*>(ts);
-  // (low id, timestamp, arrival): timestamp first, then the low id, both stable
-  LAUNCH(k_take, m, ts64, w.v[0], kSign, w.k[0], m);
-  ITRY(sort64(w, w.k[0], w.k[1], w.v[0], w.v[1], m, s));
-  LAUNCH(k_take, m, lo, w.v[1], 0ull, w.k[0], m);
-  uint32_t* const by_key = w.u[3];  // kept for the newest timestamps below
-  ITRY(sort64(w, w.k[0], w.k[1], w.v[1], by_key, m, s));
-  // storage order: (low id, first arrival of the (low id, timestamp) key, arrival)
-  LAUNCH(k_key_heads, m, lo, ts, by_key, m, w.u[0]);
-  ITRY(max_scan(w, w.u[0], w.u[1], m, s));
-  LAUNCH(k_first_seen, m, by_key, w.u[1], m, w.k[0]);
-  ITRY(sort64(w, w.k[0], w.k[1], by_key, w.v[0], m, s));
-  LAUNCH(k_take, m, lo, w.v[0], 0ull, w.k[0], m);
-  ITRY(sort64(w, w.k[0], w.k[1], w.v[0], w.v[1], m, s));
-  uint32_t* const stored = w.v[1];  // low ids ascending, storage order inside; w.k[1] = their low ids
+  uint64_t m2 = 0;
+  if (mode == SEL_NEWEST) {
+    ITRY(alive_of(w, w.bk, alive, n, n_alive, by_key, &m2, s));
+    if (m2 != m) return hipErrorUnknown;
+  }
+  LAUNCH(k_take, m, lo, stored, 0ull, w.k[1], m);  // their low ids
   uint64_t T = 0;
   if (mode == SEL_ALL) {
     ITRY(hipMemcpyAsync(perm, stored, m * 4, hipMemcpyDeviceToDevice, s));
@@ -393,20 +518,20 @@ hipError_t index_select(IndexWork& w, const uint64_t* lo, const uint64_t* hi, co
 }
 
 hipError_t index_evict(IndexWork& w, const uint64_t* lo, const int64_t* ts, uint8_t* alive, uint64_t n,
-                       uint64_t to_recover, uint64_t* evicted, bool* exhausted, hipStream_t s) {
+                       uint64_t n_alive, uint64_t to_recover, uint64_t* evicted, bool* exhausted, hipStream_t s) {
   uint64_t m = 0;
   *evicted = 0;
   *exhausted = false;
   if (to_recover == 0) return hipSuccess;
   if (n >= (1ull << 31)) return hipErrorInvalidValue;
+  ITRY(index_update(w, lo, ts, n, s));
   ITRY(reserve(w, n));  // before any w buffer is named: reserve reallocates them
-  ITRY(index_alive(w, alive, n, w.v[0], &m, s));
+  if (n_alive) ITRY(alive_of(w, w.bk, alive, n, n_alive, w.v[1], &m, s));  // by (low id, timestamp)
   if (m == 0) {
     *exhausted = true;
     return hipSuccess;
   }
-  LAUNCH(k_take, m, lo, w.v[0], 0ull, w.k[0], m);
-  ITRY(sort64(w, w.k[0], w.k[1], w.v[0], w.v[1], m, s));
+  LAUNCH(k_take, m, lo, w.v[1], 0ull, w.k[1], m);
   LAUNCH(k_runs, m, w.k[1], m, w.flag);
   uint64_t T = 0;
   ITRY(offsets_of(w, w.flag, m, w.seg, &T, s));

@@ -124,10 +124,8 @@ class JsonV2Decoder:
             out = self._dec.retry()
         n = int(out.n_spans)
         if n == 0:
-            return DecodedBatch(0, None, np.zeros(0, np.uint64), np.zeros(0, np.int64))
-        lo = np.ctypeslib.as_array(out.trace_lo, (n,)).copy()
-        ts = np.ctypeslib.as_array(out.timestamp, (n,)).copy()
-        return DecodedBatch(n, out.dev, lo, ts, out.dev_trace_hi)
+            return DecodedBatch(0, None)
+        return DecodedBatch(n, out.dev, out.dev_trace_hi, self._dec)
 
     def decode_columns(self, data: bytes) -> Columns:
         """Host columns of one decoded batch, one span per trace (as ``accept`` packs them)."""

@@ -24,11 +24,26 @@ from .model import format_ipv6
 
 @dataclass
 class DecodedBatch:
+    """A decode's result: device columns owned by the decoder until its next decode. The host
+    copies of trace_lo / timestamp are downloaded only when read (the storage facade never
+    does: accept goes device columns -> store)."""
     n_spans: int
-    dev: Optional[N.SpanCols]  # device columns owned by the decoder until its next decode
-    trace_lo: np.ndarray       # host copies
-    timestamp: np.ndarray
+    dev: Optional[N.SpanCols]
     dev_trace_hi: Optional[int] = None  # device pointer: the trace ids' high 64 bits (0 = 64-bit id)
+    _dec: Optional[N.Decoder] = None
+
+    def _host(self, name, dtype):
+        if self.n_spans == 0:
+            return np.zeros(0, dtype)
+        return self._dec.download(self.n_spans, (name,))[name]
+
+    @property
+    def trace_lo(self) -> np.ndarray:
+        return self._host("trace_lo", np.uint64)
+
+    @property
+    def timestamp(self) -> np.ndarray:
+        return self._host("timestamp", np.int64)
 
 
 def _key_string(dict_id: int, raw: bytes) -> str:
@@ -56,10 +71,8 @@ class Proto3Decoder:
             out = self._dec.retry()
         n = int(out.n_spans)
         if n == 0:
-            return DecodedBatch(0, None, np.zeros(0, np.uint64), np.zeros(0, np.int64))
-        lo = np.ctypeslib.as_array(out.trace_lo, (n,)).copy()
-        ts = np.ctypeslib.as_array(out.timestamp, (n,)).copy()
-        return DecodedBatch(n, out.dev, lo, ts, out.dev_trace_hi)
+            return DecodedBatch(0, None)
+        return DecodedBatch(n, out.dev, out.dev_trace_hi, self._dec)
 
     def decode_columns(self, data: bytes) -> Columns:
         """Host columns of one decoded batch, one span per trace (as ``accept`` packs them)."""

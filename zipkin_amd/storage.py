@@ -66,11 +66,14 @@ class InMemoryStorage:
     outnumber the live ones, so maxSpanCount bounds the footprint like the reference's."""
 
     def __init__(self, strict_trace_id: bool = True, search_enabled: bool = True,
-                 max_span_count: int = 500000, device: int = 0, compact_min: int = 1 << 16):
+                 max_span_count: int = 500000, device: int = 0, compact_min: int = 1 << 16,
+                 insertion_order: bool = True):
         """compact_min: evicted spans are released once they number more than
-        max(live spans, compact_min)."""
+        max(live spans, compact_min). insertion_order=False links the selection on the streaming
+        path and returns the links sorted by (parent, child) instead of DependencyLinker's order."""
         if max_span_count <= 0:
             raise ValueError("maxSpanCount <= 0")
+        self.insertion_order = insertion_order
         self.strict_trace_id = strict_trace_id
         self.search_enabled = search_enabled
         self.max_span_count = max_span_count
@@ -161,7 +164,7 @@ class InMemoryStorage:
         _, n_traces = self._store.select(mode)
         if n_traces == 0:
             return []
-        linker = DependencyLinker(self.device)
+        linker = DependencyLinker(self.device, insertion_order=self.insertion_order)
         linker.svc, linker.ip4, linker.ip6 = self._linker.svc, self._linker.ip4, self._linker.ip6
         try:
             ctx = linker._context(window is not None)
