@@ -293,6 +293,14 @@ int zdl_sync(zdl_ctx* ctx);
  * ZDL_ORDER_INSERTION on a ZDL_FLAG_INSERTION_ORDER context (the reference's list order). */
 int zdl_link(zdl_ctx* ctx, int order, zdl_links* out);
 
+/* zdl_link in two halves, so that the link list's trip over PCIe into the context's pinned
+ * host columns overlaps other work (e.g. the next put on another context): zdl_link_start
+ * enqueues the compaction and returns; zdl_link_finish waits for it and fills out exactly as
+ * zdl_link would. A sparse context's sorted list is compacted asynchronously; every other case
+ * computes in zdl_link_finish. Nothing else may use the context in between. */
+int zdl_link_start(zdl_ctx* ctx, int order);
+int zdl_link_finish(zdl_ctx* ctx, zdl_links* out);
+
 /* DependencyLinker.merge(links): sums call/error counts per (parent, child) of the n
  * input links, on the device; output in first-seen order (ZDL_ORDER_FIRST_SEEN).
  * Does not touch the context's accumulated counts. */

@@ -163,3 +163,27 @@ def test_messy_big_traces_vs_cpp(gmin, monkeypatch):
     assert _link(cols, w.total_services) == _oracle(cols)
     win = (base_ms + 2_000, 1_000)
     assert _link(cols, w.total_services, window=win) == _oracle(cols, window=win)
+
+
+@pytest.mark.parametrize("sparse", [True, False])
+def test_link_start_finish_equals_link(sparse, monkeypatch):
+    """zdl_link_start / zdl_link_finish (the compaction in flight while the caller does other
+    work, e.g. another context's put) return exactly zdl_link's list; a second start before the
+    finish is refused."""
+    if sparse:
+        monkeypatch.setenv("ZDL_SPARSE", "1")
+    cols = synth.generate(synth.C4.scaled(20_000))
+    S = synth.C4.total_services
+    a, b = N.Context(S), N.Context(S)
+    a.put_spans(cols)
+    b.put_spans(cols)
+    a.link_start()
+    with pytest.raises(N.ZdlError):
+        a.link_start()
+    b.put_spans(cols)  # another context's work while a's link is in flight
+    got = a.link_finish()
+    want = a.link()
+    assert all(np.array_equal(x, y) for x, y in zip(got, want)) and len(want[0]) > 0
+    assert sorted(_tuples(*got)) == _oracle(cols)
+    a.close()
+    b.close()

@@ -49,6 +49,7 @@ EXPORTS = (
     "zdl_decoder_download", "zdl_decoder_kernel_ms", "zdl_put_mysql_rows", "zdl_rows_last_error",
     "zdl_comm_unique_id", "zdl_comm_init", "zdl_put_spans_device_multi", "zdl_device_count", "zdl_shard_of",
     "zdl_tree_export", "zdl_tree_reasons", "zdl_decode_json_v2", "zdl_decode_retry", "zdl_decoder_struct_ms",
+    "zdl_link_start", "zdl_link_finish",
 )
 ZDL_ABI_VERSION = 3
 ZDL_COMM_ID_BYTES = 128
@@ -138,6 +139,8 @@ def lib() -> C.CDLL:
     L.zdl_put_spans_device.argtypes = [vp, C.POINTER(SpanCols), u64, vp, u64]
     L.zdl_sync.argtypes = [vp]
     L.zdl_link.argtypes = [vp, C.c_int, C.POINTER(Links)]
+    L.zdl_link_start.argtypes = [vp, C.c_int]
+    L.zdl_link_finish.argtypes = [vp, C.POINTER(Links)]
     L.zdl_merge_links.argtypes = [vp, vp, vp, vp, vp, u64, C.POINTER(Links)]
     L.zdl_add_links.argtypes = [vp, vp, vp, vp, vp, u64]
     L.zdl_reset.argtypes = [vp]
@@ -379,6 +382,16 @@ class Context:
         reads without a copy."""
         out = Links()
         self.check(self._L.zdl_link(self.h, int(order), C.byref(out)))
+        return self._links_to_numpy(out, copy)
+
+    def link_start(self, order: int = ZDL_ORDER_SORTED) -> None:
+        """zdl_link_start: enqueue the link list's compaction (finish with link_finish)."""
+        self.check(self._L.zdl_link_start(self.h, int(order)))
+
+    def link_finish(self, copy: bool = True):
+        """zdl_link_finish: the started link's (parent, child, call, err), as link() returns them."""
+        out = Links()
+        self.check(self._L.zdl_link_finish(self.h, C.byref(out)))
         return self._links_to_numpy(out, copy)
 
     def set_days(self, day0_ms: int, n_days: int):

@@ -96,6 +96,8 @@ struct Args {
   uint32_t* done;            // k_tail workgroups finished (the last one compacts; resets it)
   unsigned long long* flag;  // mapped pinned: k_tail's last workgroup stores `seq` after the
   unsigned long long seq;    // records (system-scope release), so zdl_link can spin on it
+  int lazy;                  // k_link's last workgroup compacts when nothing is left for k_mid /
+                             // k_tail (which the put then does not launch), else stores seq | FLAG_TAIL
   unsigned long long* prof;  // ZDL_PROF=1: k_link phase cycles (12 counters)
   uint64_t* cx_win;      // k_link -> k_tail: (base | P << 48, starts mask) per window
   uint32_t skip;         // timing-only ablation of k_link (ZDL_SKIP): 32 stream only, 64 fields,
@@ -177,6 +179,8 @@ enum : int { CTR_MID = 0, CTR_CX = 1, CTR_LARGE = 2, CTR_TICK_LARGE = 3, CTR_TIC
 constexpr int CTR_DONE = 2 * CTR_N;  // k_tail's finished-workgroup count (after both blocks)
 
 #include "zdl_full.inc"  // the full per-window emulation (k_tail's first part)
+constexpr unsigned long long FLAG_TAIL = 1ull << 62;  // lazy put: k_mid / k_tail still have work
+__device__ void lk_lazy_end(const Args& A);          // k_link's end in a lazy put (below)
 #include "zdl_link.inc"  // k_link, full_windows (need zdl_full.inc's helpers)
 #include "zdl_log.inc"   // LOG mode reduce: k_pscan, k_scatter, k_hist
 
@@ -1194,6 +1198,38 @@ __device__ __forceinline__ void compact_ordered(const unsigned long long* __rest
   }
 }
 
+// A lazy put's end, in k_link (every thread of every workgroup calls): the hand-off of k_tail's
+// compaction (MI355X_MICROARCH.md, "Valid forms", first row): each wave waits for its table
+// atomics, one lane per workgroup adds to `done`, and the workgroup whose add returns the last
+// ticket sees every count. If k_link left nothing for k_mid / k_tail (no listed big trace, no
+// queued window) it compacts the table into the mapped buffer, zeroes the next put's counter
+// slots and releases `seq` - the put is complete without launching them; otherwise it stores
+// seq | FLAG_TAIL and the host launches them (zdl_link, or the context's next call).
+__device__ void lk_lazy_end(const Args& A) {
+  __shared__ bool last, tail;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    last = __hip_atomic_fetch_add(A.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  if (threadIdx.x == 0) {
+    const uint32_t b = __hip_atomic_load(A.big_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t l = __hip_atomic_load(A.large_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t x = __hip_atomic_load(A.cx_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    tail = (b | l | x) != 0;
+  }
+  __syncthreads();
+  if (!tail) compact_ordered(A.call, A.err, A.rows * A.S, A.S, A.status, A.map);
+  __syncthreads();
+  if (!tail && threadIdx.x < CTR_N) A.ctr_next[threadIdx.x] = 0;  // k_tail's job when it runs
+  if (threadIdx.x == 0) {
+    *A.done = 0;
+    __threadfence_system();  // the records and counts are visible to the host before the flag
+    __hip_atomic_store(A.flag, tail ? (A.seq | FLAG_TAIL) : A.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 __global__ void __launch_bounds__(COMPACT_WG) k_compact_ordered(const unsigned long long* __restrict__ call,
                                                                 const unsigned long long* __restrict__ err,
                                                                 uint32_t SS, uint32_t S,
@@ -1489,6 +1525,13 @@ struct zdl_ctx {
   uint32_t lk_n = 0;
   uint32_t lk_stride = 1, lk_puts = 0;  // time every lk_stride-th put
   zdl_kernel_times times = {};
+  // a lazy put (Args::lazy): launched k_link only; k_mid / k_tail follow only if its flag says
+  // so (resolve_lazy), with the put's arguments kept here
+  bool lazy_pending = false;
+  Args lazy_A{};
+  int lazy_wmode = 0, lazy_dense = 0;
+  int link_pending = -1;  // zdl_link_start's order until zdl_link_finish (-1: none)
+  bool link_async = false;  // the started link is a sparse compaction in flight
 };
 
 namespace {
@@ -1584,6 +1627,7 @@ int group_first(zdl_ctx* g, int rc, zdl_ctx* s = nullptr) {
 }
 int group_put(zdl_ctx* g, const zdl_span_cols* col, uint64_t n_spans, const uint64_t* off, uint64_t n_traces);
 int group_export(zdl_ctx* g, void* dev_call, void* dev_err);
+static int resolve_lazy(zdl_ctx* c, bool wait);  // a lazy put's k_mid / k_tail (below)
 
 // splitmix64 finaliser (shard.py's): trace t goes to device splitmix64(trace_lo) % n
 inline uint64_t splitmix64(uint64_t x) {
@@ -1716,6 +1760,8 @@ void zdl_destroy(zdl_ctx* c) {
     return;
   }
   if (c->comm) (void)ncclCommDestroy(c->comm);
+  (void)hipSetDevice(c->device);
+  (void)resolve_lazy(c, false);
   c->red_call.release();
   c->red_err.release();
   (void)hipSetDevice(c->device);
@@ -2064,11 +2110,52 @@ static int giant_run(zdl_ctx* c, Args& A, uint64_t n_spans, uint64_t n_traces) {
   return ZDL_OK;
 }
 
+// A lazy put's k_mid / k_tail, when its k_link left them work (flag seq | FLAG_TAIL) or has not
+// finished yet (then they run after it in stream order and find what there is; k_tail compacts
+// and releases seq again). wait: spin for k_link first (zdl_link); otherwise never waits.
+static int resolve_lazy(zdl_ctx* c, bool wait) {
+  if (!c->lazy_pending) return ZDL_OK;
+  c->lazy_pending = false;
+  const volatile unsigned long long* f = c->h_flag;
+  unsigned long long v = *f;
+  for (uint32_t i = 1; wait && (v & ~FLAG_TAIL) != c->seq; ++i) {
+    if ((i & 255) == 0 && hipStreamQuery(c->stream) != hipErrorNotReady) {
+      v = *f;
+      break;
+    }
+    __builtin_ia32_pause();
+    v = *f;
+  }
+  if (v == c->seq) return ZDL_OK;  // complete: k_link's last workgroup compacted
+  Args A = c->lazy_A;
+  A.lazy = 0;
+  void* kargs[] = {&A};
+  if (A.wb_max) {
+    hipLaunchKernelGGL(k_mid, dim3((unsigned)c->cus * 4), dim3(MID_WG), 4 * WB_CARVE, c->stream, A);
+    const hipError_t me = hipGetLastError();
+    if (me != hipSuccess) {
+      c->poisoned = true;
+      return hip_fail(c, me, "k_mid launch");
+    }
+  }
+  const hipError_t le = hipLaunchKernel(k_tail_fn(c->lazy_dense, c->lazy_wmode, 0), dim3(c->grid), dim3(TAIL_WG), kargs,
+                                        tail_block_bytes(c->lazy_wmode), c->stream);
+  if (le != hipSuccess) {
+    c->poisoned = true;
+    return hip_fail(c, le, "k_tail launch");
+  }
+  return ZDL_OK;
+}
+
 // Default pipeline: k_link streams every trace of <= WSMALL spans; k_tail re-runs the
 // windows it queued, takes the traces it listed as longer than WSMALL and (small tables)
 // compacts the table into the mapped buffer zdl_link reads.
 static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans, const uint64_t* off,
                           uint64_t n_traces, const uint64_t* n_traces_dev = nullptr) {
+  {
+    const int lrc = resolve_lazy(c, false);  // the previous lazy put's k_mid / k_tail first
+    if (lrc != ZDL_OK) return lrc;
+  }
   if (c->poisoned) return fail(c, ZDL_EDEVICE, "an earlier put failed between its kernels: call zdl_reset");
   const size_t SS = (size_t)c->rows * c->S;  // table cells (days * S * S with daily buckets)
   const int dense = SS <= (size_t)wdense_max(plan_only_mode(c) ? 0 : c->window);
@@ -2240,6 +2327,11 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
     A.flag = c->d_flag;
     A.seq = c->seq + 1;
   }
+  // lazy put (small dense tables, the production k_link): k_link's last workgroup compacts when
+  // nothing is left for k_mid / k_tail, which then are not launched (resolve_lazy launches them
+  // when its flag says so)
+  static const bool nolazy = getenv("ZDL_NOLAZY") != nullptr;
+  A.lazy = A.map && tm == TM_DENSE && lmode == 0 && !nolazy && !(c->flags & ZDL_FLAG_TIMING_ALL) ? 1 : 0;
   void* kargs[] = {&A};
   ev_record(c, 0);
   ev_record(c, 1);
@@ -2263,6 +2355,18 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   }
   ev_record(c, 2);
   c->map_fresh = false;  // k_link has changed the table
+  if (A.lazy) {
+    c->lazy_A = A;
+    c->lazy_wmode = wmode;
+    c->lazy_dense = dense;
+    c->lazy_pending = true;
+    c->seq = A.seq;
+    c->span_base += n_spans;
+    ++c->epoch;  // k_link's last workgroup (or k_tail) zeroes the other counter slots
+    c->map_fresh = true;
+    c->times.grid = (uint32_t)grid;
+    return ZDL_OK;
+  }
   if (A.wb_max) {  // big_list's front (WSMALL < n <= WB_MAX spans): one wave per trace
     hipLaunchKernelGGL(k_mid, dim3((unsigned)c->cus * 4), dim3(MID_WG), 4 * WB_CARVE, c->stream, A);
     const hipError_t me = hipGetLastError();
@@ -2722,6 +2826,10 @@ int zdl_sync(zdl_ctx* c) {
   if (!c) return ZDL_EINVAL;
   if (!c->sub.empty()) return group_each(c, [&](zdl_ctx* s) { return zdl_sync(s); });
   HIP_TRY(c, enter(c));
+  {
+    const int lrc = resolve_lazy(c, false);
+    if (lrc != ZDL_OK) return lrc;
+  }
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   uint32_t st = 0;
   HIP_TRY(c, hipMemcpy(&st, c->status.p, 4, hipMemcpyDeviceToHost));
@@ -2794,6 +2902,10 @@ int zdl_reset(zdl_ctx* c) {
   if (!c) return ZDL_EINVAL;
   if (!c->sub.empty()) return group_each(c, [&](zdl_ctx* s) { return zdl_reset(s); });
   HIP_TRY(c, enter(c));
+  {
+    const int lrc = resolve_lazy(c, false);  // its counter slots must be left as k_tail leaves them
+    if (lrc != ZDL_OK) return lrc;
+  }
   if (c->poisoned) {  // the counter slots may hold a half-finished put's counts
     HIP_TRY(c, hipMemsetAsync(c->counters.p, 0, (CTR_DONE + 1) * 4, c->stream));
     c->poisoned = false;
@@ -2985,8 +3097,9 @@ static int ensure_rec(zdl_ctx* c, uint64_t m) {
 }
 
 // A sparse context's links: its sorted list (cell = id order), rank-sorted when ranks are set.
-static int link_sparse(zdl_ctx* c, zdl_links* out, const SparseTable* tab = nullptr) {
-  const SparseTable& t = tab ? *tab : c->acc;
+// The first half enqueues the compaction into the mapped host columns (zdl_link_start stops
+// there), the second waits and fills out.
+static int link_sparse_start(zdl_ctx* c, const SparseTable& t) {
   const uint64_t m = t.n;
   int rc = ensure_rec(c, m);
   if (rc != ZDL_OK) return rc;
@@ -2998,6 +3111,14 @@ static int link_sparse(zdl_ctx* c, zdl_links* out, const SparseTable* tab = null
                             (int64_t*)(c->d_rec + 16 * cap), c->stream));
   ev_record(c, 6);
   HIP_TRY(c, hipMemcpyAsync(c->h_meta, c->status.p, 16, hipMemcpyDeviceToHost, c->stream));
+  return ZDL_OK;
+}
+static int link_sparse(zdl_ctx* c, zdl_links* out, const SparseTable* tab = nullptr, bool started = false) {
+  const SparseTable& t = tab ? *tab : c->acc;
+  const uint64_t m = t.n;
+  int rc = started ? ZDL_OK : link_sparse_start(c, t);
+  if (rc != ZDL_OK) return rc;
+  const size_t cap = c->h_rec_cap;
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   rc = status_code(c, (uint32_t)c->h_meta[0]);
   if (rc != ZDL_OK) return rc;
@@ -3016,6 +3137,11 @@ extern "C" {
 int zdl_link(zdl_ctx* c, int order, zdl_links* out) {
   if (!c || !out) return ZDL_EINVAL;
   if (!c->sub.empty()) return group_link(c, order, out);
+  if (c->lazy_pending) {
+    HIP_TRY(c, enter(c));
+    const int lrc = resolve_lazy(c, true);
+    if (lrc != ZDL_OK) return lrc;
+  }
   if (c->days) return fail(c, ZDL_EINVAL, "daily buckets are set: use zdl_link_days");
   if (c->poisoned) return fail(c, ZDL_EDEVICE, "an earlier put failed between its kernels: call zdl_reset");
   if (order == ZDL_ORDER_INSERTION) {
@@ -3037,6 +3163,37 @@ int zdl_link(zdl_ctx* c, int order, zdl_links* out) {
     return link_sorted(c, c->red_call.p, c->red_err.p, false, out);
   }
   return link_sorted(c, c->call.p, c->errc.p, true, out);
+}
+
+int zdl_link_start(zdl_ctx* c, int order) {
+  if (!c) return ZDL_EINVAL;
+  if (c->link_pending >= 0) return fail(c, ZDL_EINVAL, "zdl_link_start: a started link is not finished");
+  c->link_pending = order;
+  c->link_async = false;
+  if (c->sparse && !c->comm && c->sub.empty() && order == ZDL_ORDER_SORTED && !c->poisoned) {
+    HIP_TRY(c, enter(c));
+    const int rc = link_sparse_start(c, c->acc);
+    if (rc != ZDL_OK) {
+      c->link_pending = -1;
+      return rc;
+    }
+    c->link_async = true;
+  }
+  return ZDL_OK;
+}
+
+int zdl_link_finish(zdl_ctx* c, zdl_links* out) {
+  if (!c || !out) return ZDL_EINVAL;
+  if (c->link_pending < 0) return fail(c, ZDL_EINVAL, "zdl_link_finish: no started link");
+  const int order = c->link_pending;
+  const bool started = c->link_async;
+  c->link_pending = -1;
+  c->link_async = false;
+  if (started) {
+    HIP_TRY(c, enter(c));
+    return link_sparse(c, out, nullptr, true);
+  }
+  return zdl_link(c, order, out);
 }
 
 // Daily buckets: the cells as (day, parent, child, counts), ordered like
@@ -3227,6 +3384,10 @@ int zdl_add_links(zdl_ctx* c, const int32_t* parent, const int32_t* child, const
   if (c->days) return fail(c, ZDL_EINVAL, "zdl_add_links: not with daily buckets");
   if (n == 0) return ZDL_OK;
   HIP_TRY(c, enter(c));
+  {
+    const int lrc = resolve_lazy(c, false);  // a lazy put's k_mid / k_tail before the table is used
+    if (lrc != ZDL_OK) return lrc;
+  }
   if (c->sparse) {  // merged into the sorted list (DependencyLinker.merge's sum per pair)
     std::vector<uint32_t> cells(n);
     for (uint64_t i = 0; i < n; ++i) {
@@ -3271,6 +3432,10 @@ int zdl_table_export(zdl_ctx* c, void* dev_call, void* dev_err) {
   if (!c->sub.empty()) return group_export(c, dev_call, dev_err);
   if (c->sparse) return fail(c, ZDL_EINVAL, "zdl_table_export: a sparse context has no S x S table");
   HIP_TRY(c, enter(c));
+  {
+    const int lrc = resolve_lazy(c, false);  // a lazy put's k_mid / k_tail before the table is used
+    if (lrc != ZDL_OK) return lrc;
+  }
   if (c->comm) {  // every rank's tables, summed
     const int rc = comm_sum_tables(c);
     if (rc != ZDL_OK) return rc;
@@ -3297,6 +3462,10 @@ int zdl_table_import(zdl_ctx* c, const void* dev_call, const void* dev_err) {
   if (c->ord) return fail(c, ZDL_EINVAL, "zdl_table_import: the table carries no insertion-order ranks");
   if (c->sparse) return fail(c, ZDL_EINVAL, "zdl_table_import: a sparse context has no S x S table");
   HIP_TRY(c, enter(c));
+  {
+    const int lrc = resolve_lazy(c, false);  // a lazy put's k_mid / k_tail before the table is used
+    if (lrc != ZDL_OK) return lrc;
+  }
   const size_t bytes = (size_t)c->rows * c->S * 8;
   HIP_TRY(c, hipMemcpyAsync(c->call.p, dev_call, bytes, hipMemcpyDeviceToDevice, c->stream));
   HIP_TRY(c, hipMemcpyAsync(c->errc.p, dev_err, bytes, hipMemcpyDeviceToDevice, c->stream));
@@ -3523,6 +3692,11 @@ static int group_link_sparse(zdl_ctx* g, zdl_links* out) {
 
 static int group_link(zdl_ctx* g, int order, zdl_links* out) {
   if (order != ZDL_ORDER_SORTED) return fail(g, ZDL_EINVAL, "device group: zdl_link returns ZDL_ORDER_SORTED");
+  for (zdl_ctx* s : g->sub) {  // lazy puts: their k_mid / k_tail before the tables are reduced
+    (void)hipSetDevice(s->device);
+    const int lrc = resolve_lazy(s, false);
+    if (lrc != ZDL_OK) return group_first(g, lrc, s);
+  }
   zdl_ctx* s0 = g->sub[0];
   for (size_t d = 1; d < g->sub.size(); ++d) {  // surfaces the other devices' status (NPE, bad ids)
     const int rc = zdl_sync(g->sub[d]);
@@ -3540,6 +3714,11 @@ static int group_link(zdl_ctx* g, int order, zdl_links* out) {
 
 int group_export(zdl_ctx* g, void* dev_call, void* dev_err) {
   if (g->sub[0]->sparse) return fail(g, ZDL_EINVAL, "zdl_table_export: a sparse device group has no S x S table");
+  for (zdl_ctx* s : g->sub) {
+    (void)hipSetDevice(s->device);
+    const int lrc = resolve_lazy(s, false);
+    if (lrc != ZDL_OK) return group_first(g, lrc, s);
+  }
   HIP_TRY(g, enter(g->sub[0]));
   return group_reduce(g, (unsigned long long*)dev_call, (unsigned long long*)dev_err);
 }
