@@ -26,17 +26,18 @@ Paths are relative to /root/reference/zipkin/src/main/java/zipkin2/:
                         JsonEscaper.jsonEscape
 
 Errors: every exception the reference raises while reading becomes ``IllegalArgument`` (JsonCodec
-wraps them all, :152-153, :234-239). ``Unsupported`` marks the inputs the device decoder rejects
-with ZDL_EINVAL instead of restating them: a number the reference would have to pass through
-Double.parseDouble (a fraction or exponent, ``-0`` aside, or an integer outside long/int range,
-for ``timestamp``, ``duration``, annotation ``timestamp`` and ``port``), an ip string with a
-backslash escape, and objects/arrays nested deeper than 64 inside a span.
+wraps them all, :152-153, :234-239). ``Unsupported`` marks the one input the device decoder rejects
+with ZDL_EINVAL instead of restating it: objects/arrays nested deeper than 64 inside a span. Numbers
+gson's nextLong / nextInt read through Double.parseDouble (a fraction or exponent, an integer
+outside long / int range, a quoted text Long.parseLong refuses) are restated by
+``_java_parse_double`` + ``_double_integral``; ip strings with escapes are parsed decoded.
 
 Pinned by the reference's own vectors: SpanBytesDecoderTest JSON_V2 cases and V2SpanWriterTest
 (tests/test_json_v2.py transcribes them).
 """
 from __future__ import annotations
 
+import re
 from typing import List, Optional, Tuple
 
 from zipkin_amd.model import Endpoint, Kind, Span, format_ipv6, normalize_trace_id
@@ -379,19 +380,17 @@ class _Reader:
             if v < lo or v > hi:  # nextInt: (int) peekedLong != peekedLong
                 raise IllegalArgument("NumberFormatException")
             return v
-        if p == P_NUMBER:
+        if p == P_NUMBER:  # peekedString = the number's text; then the double below
             s = self.b[self.pos:self.pos + self.number_len]
             self.pos += self.number_len
             self.peeked = P_NONE
-            if s == "-0":  # Double.parseDouble("-0") == 0 exactly
-                return 0
-            raise Unsupported(f"number {s!r} goes through Double.parseDouble")
+            return _double_integral(_java_parse_double(s), lo, hi)
         if p == P_DQ:
             self.peeked = P_NONE
             s, _ = self._quoted()
-            v = parse(s)
-            if v is None:
-                raise Unsupported(f"quoted number {s!r} goes through Double.parseDouble")
+            v = parse(s)  # Long.parseLong / Integer.parseInt first
+            if v is None:  # NumberFormatException ignored: "Fall back to parse as a double"
+                return _double_integral(_java_parse_double(s), lo, hi)
             return v
         raise IllegalArgument("Expected a long")
 
@@ -425,16 +424,93 @@ class _Reader:
                 return
 
 
+_DEC_RE = re.compile(r"(?:[0-9]+\.?[0-9]*|\.[0-9]+)(?:[eE][+-]?[0-9]+)?[fFdD]?")
+_HEX_RE = re.compile(r"[-+]?0[xX](?:[0-9a-fA-F]+\.?|[0-9a-fA-F]*\.[0-9a-fA-F]+)[pP][-+]?[0-9]+[fFdD]?")
+
+
+def _java_parse_double(s: str) -> float:
+    """Double.parseDouble (FloatingDecimal.readJavaFormatString / parseHexString): String.trim,
+    an optional sign, "NaN" / "Infinity", a hex significand with a binary exponent, or decimal
+    digits with at most one point and an optional exponent; an optional f/F/d/D suffix. The value
+    is the correctly rounded double (Python's float() and float.fromhex round the same way).
+    NumberFormatException -> IllegalArgument (JsonCodec wraps it)."""
+    i, j = 0, len(s)
+    while i < j and ord(s[i]) <= 0x20:  # String.trim
+        i += 1
+    while j > i and ord(s[j - 1]) <= 0x20:
+        j -= 1
+    t = s[i:j]
+    if not t:
+        raise IllegalArgument("NumberFormatException: empty String")
+    neg = t[0] == "-"
+    body = t[1:] if t[0] in "+-" else t
+    if body == "NaN":
+        return float("nan")
+    if body == "Infinity":
+        return float("-inf") if neg else float("inf")
+    if body[:2] in ("0x", "0X"):
+        if not _HEX_RE.fullmatch(t):
+            raise IllegalArgument(f"NumberFormatException: For input string: \"{t}\"")
+        h = t[:-1] if t[-1] in "fFdD" else t
+        try:
+            return float.fromhex(h)
+        except OverflowError:
+            return float("-inf") if neg else float("inf")
+    if not _DEC_RE.fullmatch(body):
+        raise IllegalArgument(f"NumberFormatException: For input string: \"{t}\"")
+    d = float(body[:-1] if body[-1] in "fFdD" else body)
+    return -d if neg else d
+
+
+def _double_integral(d: float, lo: int, hi: int) -> int:
+    """gson nextLong / nextInt after parseDouble: result = (long) d (or (int) d: NaN -> 0, saturating
+    at the type's bounds, otherwise toward zero); NumberFormatException when (double) result != d."""
+    if d != d:
+        r = 0
+    elif d >= hi:
+        r = hi
+    elif d <= lo:
+        r = lo
+    else:
+        r = int(d)
+    if float(r) != d:
+        raise IllegalArgument(f"NumberFormatException: Expected {'a long' if hi > 1 << 32 else 'an int'} "
+                              f"but was {d!r}")
+    return r
+
+
 def _java_parse(s: str, lo: int, hi: int) -> Optional[int]:
-    """Long.parseLong / Integer.parseInt (radix 10); None where they throw (the reference then
-    tries Double.parseDouble: Unsupported)."""
+    """Long.parseLong / Integer.parseInt (radix 10); None where they throw (gson then tries
+    Double.parseDouble)."""
     if not s:
         return None
     i = 1 if s[0] in "+-" else 0
-    if i == len(s) or not all("0" <= c <= "9" for c in s[i:]):
+    if i == len(s):
         return None
-    v = int(s)
+    v = 0
+    for c in s[i:]:
+        d = java_digit(c)
+        if d < 0:
+            return None
+        v = v * 10 + d
+    v = -v if s[0] == "-" else v
     return v if lo <= v <= hi else None
+
+
+# Character.digit(ch, 10): the Unicode decimal digits (category Nd) of the BMP, as Java 8 knows
+# them (Unicode 6.2: each block is ten consecutive code points from these starts). Newer JVMs know
+# more blocks (e.g. U+0DE6, U+A9F0 from Unicode 7): parity there is pinned to Java 8 only.
+JAVA8_DIGIT_BLOCKS = (0x30, 0x660, 0x6F0, 0x7C0, 0x966, 0x9E6, 0xA66, 0xAE6, 0xB66, 0xBE6, 0xC66, 0xCE6, 0xD66,
+                      0xE50, 0xED0, 0xF20, 0x1040, 0x1090, 0x17E0, 0x1810, 0x1946, 0x19D0, 0x1A80, 0x1A90, 0x1B50,
+                      0x1BB0, 0x1C40, 0x1C50, 0xA620, 0xA8D0, 0xA900, 0xA9D0, 0xAA50, 0xABF0, 0xFF10)
+
+
+def java_digit(c: str) -> int:
+    o = ord(c)
+    for b in JAVA8_DIGIT_BLOCKS:
+        if b <= o < b + 10:
+            return o - b
+    return -1
 
 
 # ---- Endpoint.Builder.parseIp(String) ----
@@ -582,10 +658,7 @@ def _read_endpoint(r: _Reader) -> Optional[Endpoint]:
             s = r.next_string()
             svc = None if not s else s.lower()  # toLowerCase(Locale.ROOT); non-ASCII unpinned
         elif name in ("ipv4", "ipv6"):
-            s, esc = r.next_string_raw()
-            if esc:
-                raise Unsupported("ip string with an escape")
-            ipv4, ipv6 = parse_ip(s, ipv4, ipv6)
+            ipv4, ipv6 = parse_ip(r.next_string(), ipv4, ipv6)  # the decoded text, escapes and all
         elif name == "port":
             p = r.next_int()
             if p > 0xFFFF:

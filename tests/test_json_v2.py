@@ -13,8 +13,10 @@ niceErrorOnIncomplete_annotation, niceErrorOnNull_traceId / _id / _tagValue / _a
 _annotationTimestamp, readSpan_local/remoteEndpoint_noServiceName, falseOnEmpty_inputSpans,
 niceErrorOnMalformed_inputSpans, traceRoundTrip / spansRoundTrip over the golden traces).
 Parity unpinned (no reference-executed result): non-ASCII case mapping of service names, malformed
-UTF-8 replacement counts, surrogate escapes in names; the gson restatement itself beyond those
-vectors (gson is a dependency absent from the reference tree).
+UTF-8 replacement counts, surrogate escapes in names; non-ASCII digits in quoted numbers beyond
+Java 8's table (Character.digit); the gson restatement itself beyond those vectors (gson is a
+dependency absent from the reference tree). NUMBER_VECTORS' expected values are derived from IEEE-754
+rounding and Java's cast rules, not from a run of the reference.
 """
 import random
 
@@ -172,8 +174,66 @@ def test_gson_strictness():
     assert J.read_list(b'[{"traceId":"1","id":"2","shared":tRuE}] trailing') == \
         [Span.create("1", "2", shared=True)]
     assert J.read_list(b'[{"trace\\u0049d":123,"id":"2","timestamp":"77"}]') == [Span.create("123", "2", timestamp=77)]
-    with pytest.raises(J.Unsupported):
+    with pytest.raises(J.IllegalArgument):  # nextLong: (long) 1.5 != 1.5
         J.read_list(b'[{"traceId":"1","id":"2","timestamp":1.5}]')
+
+
+# gson 2.8.5 nextLong / nextInt on PEEKED_NUMBER or a quoted text Long.parseLong refuses:
+# Double.parseDouble, (long) of it, NumberFormatException unless (double) result == the double.
+# Expected values follow from the IEEE-754 double nearest each text (Java's parseDouble rounds
+# correctly) and Java's saturating (long) / (int) casts. None = IllegalArgumentException.
+_P5 = str(5 ** 1075)  # 2^-1075 = 5^1075 / 10^1075, 752 significant digits
+_TWO_M1075 = _P5[0] + "." + _P5[1:] + "e-324"
+NUMBER_VECTORS = [
+    ("1.472470996199E15", 1472470996199000), ("1.472470996199e+15", 1472470996199000),
+    ("147247099619900E1", 1472470996199000), ("1.5", None), ("-1.5", None), ("1.0", 1), ("1e0", 1),
+    ("0.5", None), ("0.0", 0), ("-0", 0), ("-0.0", 0), ("0e7", 0), ("1e19", None), ("1E-400", 0),
+    ("9223372036854775807", 9223372036854775807),  # PEEKED_LONG
+    ("9223372036854775808", 9223372036854775807),  # 2^63: (long) saturates, (double) Long.MAX == 2^63
+    ("9223372036854776832", 9223372036854775807),  # the tie above 2^63 rounds to 2^63 (even)
+    ("9223372036854776833", None), ("9223372036854777000", None),
+    ("-9223372036854775809", -9223372036854775808), ("-9223372036854777856", None),
+    ("0.99999999999999999", 1), ("0.999999999999999944488848768742172978818416595458984375", 1),
+    ("0.999999999999999944488848768742172978818416595458984374", None),
+    ("4503599627370497.4", 4503599627370497), ("4503599627370496.5", 4503599627370496),
+    ("4503599627370497.5", 4503599627370498), ("9007199254740993", 9007199254740993),  # PEEKED_LONG
+    ("9007199254740993.0", 9007199254740992), ("9007199254740995.0", 9007199254740996), ("2.5000000000000000000001", None),
+    ("3.0000000000000004", None), ("3.0000000000000002", 3), ("3.00000000000000022204460492503130808472633361816406", 3),
+    ("3.00000000000000022204460492503130808472633361816407", None),
+    (_TWO_M1075, 0),  # 2^-1075 exactly: the tie rounds to 0 (even)
+    (_TWO_M1075[:-5] + "1e-324", None),  # just above 2^-1075: the smallest subnormal
+    ("2.4703282292062327e-324", 0), ("-1e-330", 0),
+    ('"77"', 77), ('"+77"', 77), ('"-0"', 0), ('"1.472470996199E15"', 1472470996199000), ('" 12\t"', 12),
+    ('"12d"', 12), ('"12.0F"', 12), ('"0x1p4"', 16), ('"0X1.8P1"', 3), ('"-0x.8p1"', -1), ('"0x8.p-3"', 1),
+    ('"0x1p63"', 9223372036854775807), ('"-0x1p63"', -9223372036854775808), ('"0x1p64"', None),
+    ('"0x1.00000000000008p52"', 4503599627370496), ('"0x1.00000000000018p52"', 4503599627370498),
+    ('"0x1p-1075"', 0), ('"0x1.0000001p-1075"', None), ('"0x1p-1076"', 0), ('"0x0p99999999999"', 0),
+    ('"\u0031\u0032"', 12), ('"\u0661\u0662"', 12), ('"\uff11"', 1), ('"\u0de7"', None),  # Java 8 digits only
+    ('"NaN"', None), ('"Infinity"', None), ('"-Infinity"', None), ('"1e"', None), ('"1e+"', None),
+    ('"1.2.3"', None), ('""', None), ('"+"', None), ('"."', None), ('".5"', None), ('"5."', 5), ('"1_0"', None),
+    ('"0x1"', None), ('"0x"', None), ('"1d "', 1), ('"1dd"', None), ('"1 d"', None), ('"٣.0"', None),
+    ("01", None), ("1.", None), ("-", None), (".5", None), ("1e", None),
+]
+
+
+def _read_ts(text):
+    try:
+        return J.read_list(('[{"traceId":"1","id":"2","timestamp":%s}]' % text).encode())[0].timestamp
+    except J.IllegalArgument:
+        return None
+
+
+@pytest.mark.parametrize("text,exp", NUMBER_VECTORS)
+def test_next_long_through_parse_double(text, exp):
+    got = _read_ts(text)
+    assert got == (None if exp is None else max(exp, 0))  # Span.Builder.timestamp drops negatives
+    # nextInt (port): the same double, (int) cast
+    try:
+        (s,) = J.read_list(('[{"traceId":"1","id":"2","localEndpoint":{"port":%s}}]' % text).encode())
+        port = s.local_endpoint.port if s.local_endpoint else 0
+        assert exp is not None and -(1 << 31) <= exp <= 0xFFFF and port == max(exp, 0)
+    except J.IllegalArgument:
+        assert exp is None or not (-(1 << 31) <= exp <= 0xFFFF)
 
 
 # ---------------- generators: gson-legal formatting variety ----------------
@@ -212,17 +272,34 @@ def _endpoint(r, e: Endpoint) -> str:
         svc = "".join(c.upper() if r.random() < 0.3 else c for c in e.service_name)
         m.append(('"serviceName"', _esc_some(r, svc)))
     if e.ipv4 is not None:
-        m.append(('"ipv4"' if r.random() < 0.8 else '"ipv6"', '"%s"' % e.ipv4))
+        v4 = e.ipv4 if r.random() < 0.9 else "::ffff:" + e.ipv4
+        m.append(('"ipv4"' if r.random() < 0.8 else '"ipv6"', _esc_some(r, v4) if r.random() < 0.2 else '"%s"' % v4))
     if e.ipv6 is not None:
-        m.append(('"ipv6"', '"%s"' % (e.ipv6.upper() if r.random() < 0.3 else e.ipv6)))
+        v6 = e.ipv6.upper() if r.random() < 0.3 else e.ipv6
+        m.append(('"ipv6"', _esc_some(r, v6) if r.random() < 0.2 else '"%s"' % v6))
     if e.port:
-        m.append(('"port"', str(e.port) if r.random() < 0.8 else '"%d"' % e.port))
+        m.append(('"port"', _num_text(r, e.port)))
     if r.random() < 0.2:
         m.append(('"serviceName"' if not e.service_name else '"extra"', _kw(r, "null")))
     if r.random() < 0.2:
         m.append(('"whatever"', _junk_value(r)))
     r.shuffle(m)
     return "{" + ",".join(_ws(r) + k + _ws(r) + ":" + _ws(r) + v + _ws(r) for k, v in m) + "}"
+
+
+def _num_text(r, v: int) -> str:
+    """An integer as some text gson's nextLong / nextInt reads as v."""
+    k = r.randrange(10)
+    if k < 6:
+        return str(v)
+    if k == 6:
+        return '"%d"' % v
+    d = str(v)
+    if k == 7:  # exact scientific notation
+        return ("%s.%sE%d" % (d[0], d[1:], len(d) - 1)) if len(d) > 1 else d + ".0e0"
+    if k == 8:
+        return d + "." + "0" * r.randrange(1, 4)
+    return '"%s"' % (d + r.choice(["d", "D", ".0f", " "]))
 
 
 def noisy_span(r, s: Span) -> str:
@@ -237,15 +314,15 @@ def noisy_span(r, s: Span) -> str:
     if s.name:
         m.append(('"name"', _esc_some(r, s.name)))
     if s.timestamp:
-        m.append(('"timestamp"', str(s.timestamp) if r.random() < 0.8 else '"%d"' % s.timestamp))
+        m.append(('"timestamp"', _num_text(r, s.timestamp)))
     if s.duration:
-        m.append(('"duration"', str(s.duration)))
+        m.append(('"duration"', _num_text(r, s.duration)))
     if s.local_endpoint:
         m.append(('"localEndpoint"', _endpoint(r, s.local_endpoint)))
     if s.remote_endpoint:
         m.append(('"remoteEndpoint"', _endpoint(r, s.remote_endpoint)))
     if s.annotations:
-        m.append(('"annotations"', "[" + ",".join('{"value":%s,"timestamp":%d}' % (_esc_some(r, v), t)
+        m.append(('"annotations"', "[" + ",".join('{"value":%s,"timestamp":%s}' % (_esc_some(r, v), _num_text(r, t))
                                                   for t, v in s.annotations) + "]"))
     if s.tags:
         m.append(('"tags"', "{" + ",".join(_esc_some(r, k) + ":" + _esc_some(r, v) for k, v in s.tags) + "}"))
@@ -389,7 +466,63 @@ def test_gpu_decode_errors_match_oracle():
             assert_same(dec.decode_columns(data), exp)
             assert [x.strings for x in d] == [x.strings for x in o]
         dec.close()
-    assert min(seen.values()) > 0, seen
+    assert seen["ok"] > 0 and seen["iae"] > 0, seen  # "unsupported": nesting > 64 only, rare here
+
+
+@pytest.mark.gpu
+def test_gpu_numbers_through_parse_double():
+    """NUMBER_VECTORS and random texts near the rounding boundaries as timestamp, duration,
+    annotation timestamp and port: the device accepts, rejects and reads them like the oracle."""
+    from zipkin_amd import _native as N
+    r = random.Random(3)
+    texts = [t for t, _ in NUMBER_VECTORS]
+    for _ in range(400):
+        texts.append(_edge_number(r))
+    dec = _dec(fresh())
+    o = fresh()
+    fields = ['"timestamp":%s', '"duration":%s', '"annotations":[{"value":"a","timestamp":%s}]',
+              '"localEndpoint":{"serviceName":"s","port":%s}']
+    n_ok = 0
+    for text in texts:
+        for f in fields:
+            data = ('[{"traceId":"1","id":"2",' + f % text + '}]').encode()
+            try:
+                exp = oracle_columns(data, *o)
+            except J.IllegalArgument:
+                with pytest.raises(N.ReferenceIllegalArgumentException):
+                    dec.decode_columns(data)
+                continue
+            assert_same(dec.decode_columns(data), exp)
+            n_ok += 1
+    assert n_ok > 300
+    dec.close()
+
+
+def _edge_number(r) -> str:
+    """A number text near a rounding boundary of the doubles nextLong / nextInt meet."""
+    base = r.choice([r.randrange(1 << 40), (1 << 52) + r.randrange(-3, 4), (1 << 53) + r.randrange(-3, 4),
+                     (1 << 63) + r.randrange(-3000, 3000), (1 << 31) + r.randrange(-3, 3), r.randrange(100)])
+    sign = "-" if r.random() < 0.2 else ""
+    k = r.randrange(7)
+    if k == 0:
+        t = "%d.%s" % (base, r.choice(["5", "49999999999999999999", "50000000000000000001", "0", "25", "75"]))
+    elif k == 1:
+        d = str(base)
+        t = "%s.%se%d" % (d[0], d[1:] or "0", len(d) - 1 + r.randrange(-2, 3))
+    elif k == 2:
+        t = "%de%d" % (base, r.randrange(-5, 5))
+    elif k == 3:
+        t = "0.%s" % ("9" * r.randrange(10, 25) + r.choice(["", "4", "5", "44488848768742172978818416595458984375"]))
+    elif k == 4:
+        t = "%s1e-%d" % (sign, r.randrange(300, 400))
+        sign = ""
+    elif k == 5:
+        t = "0x%xp%d" % (base, r.randrange(-8, 12))
+        return '"' + sign + t + r.choice(["", "d", "F"]) + '"'
+    else:
+        t = str(base)
+    t = sign + t
+    return t if r.random() < 0.7 else '"%s%s%s"' % (r.choice(["", " ", "\\t"]), t, r.choice(["", "d", " "]))
 
 
 @pytest.mark.gpu

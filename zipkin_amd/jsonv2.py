@@ -6,12 +6,13 @@ internal/V2SpanReader.java:25-135 over gson 2.8.5's strict JsonReader (paths und
 (zipkin_amd/csrc/zdl_json.inc); this module only owns the dictionaries. When the device meets a
 key its table lacks it lists it, and the key is normalised here the way the reference's builders
 do — a service name's JSON text unescaped (gson readEscapeCharacter) and lower-cased
-(Endpoint.Builder.serviceName, Endpoint.java:132-136); an ipv4 text kept as given
-(Endpoint.java:222-227); an ipv6 text parsed to its 16 bytes (textToNumericFormatV6,
+(Endpoint.Builder.serviceName, Endpoint.java:132-136); an ipv4 text kept as given, unescaped
+(Endpoint.java:222-227); an ipv6 text unescaped, parsed to its 16 bytes (textToNumericFormatV6,
 Endpoint.java:417-487) and written back by writeIpV6 (:350-407) — given the id of its string in
 first-seen order (the ids ``columnar.pack_traces`` assigns to the decoded spans) and bound, and the
 kernel re-runs on the resident batch. Malformed input raises like the reference
-(IllegalArgumentException); inputs the decoder does not restate raise ZdlError (ZDL_EINVAL).
+(IllegalArgumentException); the one input the decoder does not restate (objects or arrays nested deeper than 64
+inside a span) raises ZdlError (ZDL_EINVAL).
 """
 from __future__ import annotations
 
@@ -107,9 +108,10 @@ class JsonV2Decoder:
         if dict_id == N.ZDL_DICT_JSON_SERVICE:
             self._dec.bind(dict_id, raw, self.svc.id(unescape(raw).lower()))  # non-ASCII case mapping unpinned
         elif dict_id == N.ZDL_DICT_JSON_IPV4:
-            self._dec.bind(dict_id, raw, self.ip4.id(raw.decode("ascii")))
+            t = unescape(raw)  # the device lists an escaped text whole: keep the IPv4 after any ':'
+            self._dec.bind(dict_id, raw, self.ip4.id(t[t.rfind(":") + 1:]))
         elif dict_id == N.ZDL_DICT_JSON_IPV6TEXT:
-            b = ipv6_bytes(raw.decode("ascii"))
+            b = ipv6_bytes(unescape(raw))
             if b is None:  # the device only lists texts it parsed
                 raise N.ZdlError(N.ZDL_EINVAL, f"ipv6 text {raw!r} does not parse")
             self._dec.bind(N.ZDL_DICT_IPV6, b, self.ip6.id(format_ipv6(b)))
