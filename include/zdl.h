@@ -36,8 +36,9 @@
 extern "C" {
 #endif
 
-#define ZDL_ABI_VERSION 3  /* 2: zdl_config.n_devices / device_ids, RCCL combine; 3: zdl_kernel_times
-                              per phase of a put (mid_ms, giant_ms, sparse_ms) */
+#define ZDL_ABI_VERSION 4  /* 2: zdl_config.n_devices / device_ids, RCCL combine; 3: zdl_kernel_times
+                              per phase of a put (mid_ms, giant_ms, sparse_ms); 4: trace id widths
+                              (zdl_store_append_ids, zdl_decoded.dev_trace_wide) */
 
 /* ---- status codes ---- */
 #define ZDL_OK          0
@@ -218,6 +219,13 @@ int         zdl_store_append(zdl_store* store, const zdl_span_cols* cols, uint64
 /* zdl_store_append with the high 64 bits of each span's trace id (NULL = all 0). */
 int         zdl_store_append_traced(zdl_store* store, const zdl_span_cols* cols, const uint64_t* trace_hi,
                                     uint64_t n_spans);
+/* ... and each trace id's width (1 = 128-bit: Span.normalizeTraceId gave 32 hex characters, which
+ * a 17-31 character id does even when its high half is zero; 0 = 64-bit). trace_wide NULL:
+ * 128-bit exactly when trace_hi != 0 (true for every id a proto3 decoder reads). The strict
+ * no-argument getDependencies() groups by (low, high, width): the reference's strictByTraceId
+ * compares the normalized strings (InMemoryStorage.java:241-262). */
+int         zdl_store_append_ids(zdl_store* store, const zdl_span_cols* cols, const uint64_t* trace_hi,
+                                 const uint8_t* trace_wide, uint64_t n_spans);
 int         zdl_store_clear(zdl_store* store);
 /* Keeps the stored spans keep[0..n_keep) (ascending positions), in that order, and frees the
  * rest, in one device gather. Positions are renumbered 0..n_keep). */
@@ -398,6 +406,8 @@ typedef struct zdl_decoded {
   uint64_t        n_missing;  /* > 0: bind the keys, then zdl_decode_proto3_retry */
   const uint64_t* dev_trace_hi; /* device: each span's trace id high 64 bits (0 = 64-bit id), for
                                    zdl_store_append_traced */
+  const uint8_t*  dev_trace_wide; /* device: each trace id's width (1 = 128-bit), for
+                                     zdl_store_append_ids; NULL: 128-bit iff dev_trace_hi != 0 */
 } zdl_decoded;
 zdl_decoder* zdl_decoder_create(int device);
 void         zdl_decoder_destroy(zdl_decoder* dec);

@@ -4,6 +4,7 @@ accept appends to HBM once, eviction (IMS:184-211) and getDependencies' trace or
 Compared, exactly (list order included), with the oracle's InMemoryStorage
 (oracle/dl_oracle.py), itself pinned by the ITDependencies / InMemoryStorageTest vectors."""
 import random
+import re
 
 import numpy as np
 import pytest
@@ -101,7 +102,10 @@ def _mixed_width_batches(seed, n_batches=5):
             hi = format(r.getrandbits(64) | 1, "016x")
             ts0 = BASE_US + r.randrange(10_000_000_000)
             for s in random_trace(r, allow_npe=False):
-                tid = hi + lo if r.random() < 0.6 else lo
+                # 128-bit, 64-bit, or 17-31 digits: padded to 32 characters with a zero high half,
+                # which strictByTraceId still tells from the 16-character id (Span.java:634-649)
+                x = r.random()
+                tid = hi + lo if x < 0.5 else lo if x < 0.8 else "0" * r.randint(1, 15) + lo
                 batch.append(s.to_builder(trace_id=tid, timestamp=ts0 + r.randrange(1_000_000)))
         r.shuffle(batch)
         out.append(batch)
@@ -249,18 +253,23 @@ def test_decoded_ingest_evicts_like_accept(fmt, seed):
 @pytest.mark.parametrize("fmt", ["proto3", "json_v2"])
 @pytest.mark.parametrize("seed", range(6))
 def test_decoded_ingest_strict_no_arg_get_dependencies(fmt, seed):
-    """The decoders keep the trace ids' high 64 bits on the device (zdl_decoded.dev_trace_hi),
-    so getDependencies() with strictTraceId splits decoded spans like accept'ed ones."""
+    """The decoders keep the trace ids' high 64 bits and widths on the device
+    (zdl_decoded.dev_trace_hi / dev_trace_wide), so getDependencies() with strictTraceId splits
+    decoded spans like accept'ed ones (JSON ids of 17-31 digits included)."""
     from oracle import json_oracle as J
     from oracle import proto3_oracle as P
     write = P.write_list if fmt == "proto3" else J.write_list
     read = (lambda d: P.read_list(d)[0]) if fmt == "proto3" else J.read_list
     store = InMemoryStorage(strict_trace_id=True, max_span_count=80, compact_min=4)
     ref = O.InMemoryStorage(strict_trace_id=True, max_span_count=80)
+    rr = random.Random(seed)
     for b in _mixed_width_batches(200 + seed):
         if len(b) > 80:
             continue
         data = write(b)
+        if fmt == "json_v2":  # some ids as 17-31 digits: 128-bit after normalizeTraceId, high half zero
+            data = re.sub(rb'"traceId":"0{16}([0-9a-f]{16})"', lambda m: b'"traceId":"' + b"0" * rr.randint(0, 15)
+                          + m.group(1) + b'"', data)
         (store.accept_proto3 if fmt == "proto3" else store.accept_json_v2)(data).execute()
         ref.accept(read(data))
         try:

@@ -42,7 +42,7 @@ EXPORTS = (
     "zdl_link", "zdl_merge_links", "zdl_add_links", "zdl_reset", "zdl_table_export",
     "zdl_table_import", "zdl_get_kernel_times", "zdl_stream", "zdl_set_days", "zdl_link_days",
     "zdl_store_create", "zdl_store_destroy", "zdl_store_last_error", "zdl_store_append", "zdl_store_clear",
-    "zdl_store_size", "zdl_put_stored", "zdl_store_compact", "zdl_store_append_traced", "zdl_store_alive",
+    "zdl_store_size", "zdl_put_stored", "zdl_store_compact", "zdl_store_append_traced", "zdl_store_append_ids", "zdl_store_alive",
     "zdl_store_evict", "zdl_store_compact_evicted", "zdl_store_select", "zdl_store_selection", "zdl_put_selection",
     "zdl_decoder_create", "zdl_decoder_destroy", "zdl_decoder_last_error", "zdl_decoder_bind",
     "zdl_decoder_dict_size", "zdl_decoder_missing", "zdl_decode_proto3", "zdl_decode_proto3_retry",
@@ -51,7 +51,7 @@ EXPORTS = (
     "zdl_tree_export", "zdl_tree_reasons", "zdl_decode_json_v2", "zdl_decode_retry", "zdl_decoder_struct_ms",
     "zdl_link_start", "zdl_link_finish",
 )
-ZDL_ABI_VERSION = 3
+ZDL_ABI_VERSION = 4
 ZDL_COMM_ID_BYTES = 128
 
 
@@ -91,7 +91,8 @@ class MysqlRows(C.Structure):
 
 class Decoded(C.Structure):
     _fields_ = [("n_spans", C.c_uint64), ("dev", SpanCols), ("trace_lo", C.POINTER(C.c_uint64)),
-                ("timestamp", C.POINTER(C.c_int64)), ("n_missing", C.c_uint64), ("dev_trace_hi", C.c_void_p)]
+                ("timestamp", C.POINTER(C.c_int64)), ("n_missing", C.c_uint64), ("dev_trace_hi", C.c_void_p),
+                ("dev_trace_wide", C.c_void_p)]
 
 
 class KernelTimes(C.Structure):
@@ -164,6 +165,8 @@ def lib() -> C.CDLL:
     L.zdl_store_size.restype = u64
     L.zdl_store_append_traced.argtypes = [vp, C.POINTER(SpanCols), vp, u64]
     L.zdl_store_append_traced.restype = C.c_int
+    L.zdl_store_append_ids.argtypes = [vp, C.POINTER(SpanCols), vp, vp, u64]
+    L.zdl_store_append_ids.restype = C.c_int
     L.zdl_store_alive.argtypes = [vp]
     L.zdl_store_alive.restype = u64
     L.zdl_store_evict.argtypes = [vp, u64, C.POINTER(u64)]
@@ -465,18 +468,22 @@ class Store:
         if rc != ZDL_OK:
             raise ZdlError(rc, self._L.zdl_store_last_error(self.h).decode())
 
-    def append_device(self, dev: SpanCols, n: int, trace_hi: Optional[int] = None) -> None:
+    def append_device(self, dev: SpanCols, n: int, trace_hi: Optional[int] = None,
+                      trace_wide: Optional[int] = None) -> None:
         """Appends device columns (e.g. a Decoder's output, trace_lo included) without a host
-        round trip; trace_hi: device pointer to the high trace ids (None = all 0)."""
-        self._check(self._L.zdl_store_append_traced(self.h, C.byref(dev), trace_hi, int(n)))
+        round trip; trace_hi / trace_wide: device pointers to the high trace ids (None = all 0)
+        and the ids' widths (None = 128-bit iff the high half is non-zero)."""
+        self._check(self._L.zdl_store_append_ids(self.h, C.byref(dev), trace_hi, trace_wide, int(n)))
 
-    def append(self, cols, trace_hi: Optional[np.ndarray] = None) -> None:
-        """Appends host columns with their trace ids (trace_hi: high 64 bits, None = 0)."""
+    def append(self, cols, trace_hi: Optional[np.ndarray] = None, trace_wide: Optional[np.ndarray] = None) -> None:
+        """Appends host columns with their trace ids (trace_hi: high 64 bits, None = 0;
+        trace_wide: 1 for an id normalized to 32 hex characters, None = where trace_hi != 0)."""
         hi = None if trace_hi is None else np.ascontiguousarray(trace_hi, np.uint64)
+        wd = None if trace_wide is None else np.ascontiguousarray(trace_wide, np.uint8)
         sc = SpanCols(_ptr(cols.trace_lo), _ptr(cols.id), _ptr(cols.parent_id), _ptr(cols.local_svc),
                       _ptr(cols.remote_svc), _ptr(cols.local_ip4), _ptr(cols.local_ip6), _ptr(cols.port_flags),
                       _ptr(cols.timestamp))
-        self._check(self._L.zdl_store_append_traced(self.h, C.byref(sc), _ptr(hi), cols.n_spans))
+        self._check(self._L.zdl_store_append_ids(self.h, C.byref(sc), _ptr(hi), _ptr(wd), cols.n_spans))
 
     def clear(self) -> None:
         self._L.zdl_store_clear(self.h)

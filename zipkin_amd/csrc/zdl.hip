@@ -2502,6 +2502,15 @@ __global__ void k_gather_index(const uint64_t* __restrict__ lo, const uint64_t* 
   alive_o[i] = alive[j];
 }
 
+// The alive bytes of appended spans: 1, | 2 when the trace id is 128-bit (normalized to 32 hex
+// characters) - from the caller's width bytes (already copied here) or else from hi != 0
+__global__ void k_alive_init(uint8_t* __restrict__ alive, const uint64_t* __restrict__ hi, int from_wide, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const bool w = from_wide ? alive[i] != 0 : (hi != nullptr && hi[i] != 0);
+  alive[i] = (uint8_t)(w ? 3u : 1u);
+}
+
 // Keeps the stored spans idx[0..n_keep) (device, ascending) and frees the rest.
 hipError_t store_compact_dev(zdl_store* st, const uint32_t* idx, uint64_t n_keep) {
   const hipStream_t s = st->stream;
@@ -2624,7 +2633,8 @@ int zdl_store_clear(zdl_store* st) {
   return ZDL_OK;
 }
 
-int zdl_store_append_traced(zdl_store* st, const zdl_span_cols* col, const uint64_t* trace_hi, uint64_t n) {
+int zdl_store_append_ids(zdl_store* st, const zdl_span_cols* col, const uint64_t* trace_hi, const uint8_t* trace_wide,
+                         uint64_t n) {
   if (!st || !col) return ZDL_EINVAL;
   if (n == 0) return ZDL_OK;
   if (!col->id || !col->parent_id || !col->local_svc || !col->remote_svc || !col->local_ip4 || !col->local_ip6 ||
@@ -2666,7 +2676,13 @@ int zdl_store_append_traced(zdl_store* st, const zdl_span_cols* col, const uint6
   if (e == hipSuccess)
     e = col->timestamp ? hipMemcpyAsync(st->ts.p + o, col->timestamp, n * 8, hipMemcpyDefault, s)
                        : hipMemsetAsync(st->ts.p + o, 0, n * 8, s);
-  if (e == hipSuccess) e = hipMemsetAsync(st->alive.p + o, 1, n, s);
+  // alive bytes: 1, | 2 for a 128-bit trace id (the strict grouping's width bit)
+  if (e == hipSuccess && trace_wide) e = hipMemcpyAsync(st->alive.p + o, trace_wide, n, hipMemcpyDefault, s);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_alive_init, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, st->alive.p + o,
+                       trace_hi ? st->hi.p + o : nullptr, trace_wide ? 1 : 0, n);
+    e = hipGetLastError();
+  }
   // the resident trace index takes the batch in (sorted, merged: the TreeMap inserts of
   // InMemoryStorage.accept, IMS:156-181), so a query only filters and orders traces
   if (e == hipSuccess) e = zdl::index_update(st->iw, st->lo.p, st->ts.p, st->n + n, s);
@@ -2678,8 +2694,12 @@ int zdl_store_append_traced(zdl_store* st, const zdl_span_cols* col, const uint6
   return ZDL_OK;
 }
 
+int zdl_store_append_traced(zdl_store* st, const zdl_span_cols* col, const uint64_t* trace_hi, uint64_t n) {
+  return zdl_store_append_ids(st, col, trace_hi, nullptr, n);
+}
+
 int zdl_store_append(zdl_store* st, const zdl_span_cols* col, uint64_t n) {
-  return zdl_store_append_traced(st, col, nullptr, n);
+  return zdl_store_append_ids(st, col, nullptr, nullptr, n);
 }
 
 int zdl_store_compact(zdl_store* st, const uint32_t* keep, uint64_t n_keep) {

@@ -80,6 +80,7 @@ struct Out {
   unsigned long long* first_err;  // min over failing spans of (span << 1 | (iae ? 1 : 0))
   uint32_t* any_miss;
   uint64_t* trace_hi;  // the trace id's high 64 bits (0 for a 64-bit id)
+  uint8_t* trace_wide;  // JSON: 1 when Span.normalizeTraceId gives 32 characters (null for proto3)
 };
 
 enum : int { SLOT_LSVC = 0, SLOT_LIP4 = 1, SLOT_LIP6 = 2, SLOT_RSVC = 3 };
@@ -551,6 +552,7 @@ struct zdl_decoder {
   DBuf<uint32_t> pf;
   DBuf<int64_t> ts;
   DBuf<uint8_t> miss;
+  DBuf<uint8_t> wide;  // JSON: trace id widths (zdl_decoded.dev_trace_wide)
   DBuf<uint64_t> miss_off;
   DBuf<uint32_t> miss_len;
   DBuf<unsigned long long> status;  // [0] first_err, [1] any_miss (u32 in the low half)
@@ -628,7 +630,7 @@ int run_kernel(zdl_decoder* d, zdl_decoded* out) {
     Dict dict{d->slots.p, d->arena.p, d->cap ? d->cap - 1 : 0};
     Out o{d->lo.p,   d->id.p, d->pid.p, d->lsvc.p,     d->rsvc.p,     d->ip4.p,    d->ip6.p,
           d->pf.p,   d->ts.p, d->miss.p, d->miss_off.p, d->miss_len.p, d->status.p, (uint32_t*)(d->status.p + 1),
-          d->hi.p};
+          d->hi.p, d->fmt == 1 ? d->wide.p : nullptr};
     DEC_TRY(d, hipEventRecord(d->ev[0], s));
     if (d->fmt == 1)
       zjs::k_js_spans<<<(unsigned)((n + zjs::kSpanWG - 1) / zjs::kSpanWG), zjs::kSpanWG, 0, s>>>(
@@ -646,8 +648,7 @@ int run_kernel(zdl_decoder* d, zdl_decoded* out) {
       return (fe & 1) ? dfail(d, ZDL_EREF_IAE, "reference throws IllegalArgumentException reading List<Span> from json (span " +
                                                    std::to_string(fe >> 2) + ((fe & 2) ? ", after it)" : ")"))
                       : dfail(d, ZDL_EINVAL, "json v2: span " + std::to_string(fe >> 2) +
-                                                 " holds a number the reference parses through Double.parseDouble, an ip "
-                                                 "with an escape or nesting deeper than 64 (not supported)");
+                                                 " nests objects or arrays deeper than 64 (not supported)");
     if (fe != kNoErr)  // the first failing span decides, before the scan's own verdict
       return (fe & 1) ? dfail(d, ZDL_EREF_IAE, "reference throws IllegalArgumentException reading List<Span> from proto3 (span " +
                                                    std::to_string(fe >> 1) + ")")
@@ -694,6 +695,7 @@ int run_kernel(zdl_decoder* d, zdl_decoded* out) {
   out->dev = zdl_span_cols{d->lo.p, d->id.p, d->pid.p, d->lsvc.p, d->rsvc.p, d->ip4.p, d->ip6.p, d->pf.p, d->ts.p, nullptr};
   out->trace_lo = nullptr;
   out->dev_trace_hi = d->hi.p;
+  out->dev_trace_wide = d->fmt == 1 ? d->wide.p : nullptr;  // proto3: 128-bit iff the high half is non-zero
   out->timestamp = nullptr;
   return ZDL_OK;
 }
@@ -925,6 +927,7 @@ int zdl_decode_json_v2(zdl_decoder* d, const uint8_t* data, uint64_t len, zdl_de
   d->n = n;
   DEC_TRY(d, d->lo.ensure(n));
   DEC_TRY(d, d->hi.ensure(n));
+  DEC_TRY(d, d->wide.ensure(n));
   DEC_TRY(d, d->id.ensure(n));
   DEC_TRY(d, d->pid.ensure(n));
   DEC_TRY(d, d->lsvc.ensure(n));

@@ -59,6 +59,13 @@ __global__ void k_take2(const uint64_t* __restrict__ src, const uint32_t* __rest
   if (i < m) key[i] = src[outer[inner[i]]];
 }
 
+// key[i] = the 128-bit-id bit of span idx[i] (alive bit 1)
+__global__ void k_wide_key(const uint8_t* __restrict__ alive, const uint32_t* __restrict__ idx,
+                           uint32_t* __restrict__ key, uint64_t m) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < m) key[i] = (alive[idx[i]] >> 1) & 1u;
+}
+
 __global__ void k_iota32(uint32_t* __restrict__ out, uint64_t m) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < m) out[i] = (uint32_t)i;
@@ -114,14 +121,17 @@ __global__ void k_runs(const uint64_t* __restrict__ key, uint64_t m, uint8_t* __
 }
 
 // flag[i] = a trace starts at position i of perm (low id changes; or high id, when given)
+// (alive: bit 1 = the trace id is 128-bit, normalized to 32 hex characters; with hi, the strict
+// grouping's key)
 __global__ void k_trace_heads(const uint64_t* __restrict__ lo, const uint64_t* __restrict__ hi,
-                              const uint32_t* __restrict__ perm, uint64_t m, uint8_t* __restrict__ flag) {
+                              const uint8_t* __restrict__ alive, const uint32_t* __restrict__ perm, uint64_t m,
+                              uint8_t* __restrict__ flag) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= m) return;
   bool h = i == 0;
   if (!h) {
     const uint32_t a = perm[i - 1], b = perm[i];
-    h = lo[a] != lo[b] || (hi && hi[a] != hi[b]);
+    h = lo[a] != lo[b] || (hi && (hi[a] != hi[b] || ((alive[a] ^ alive[b]) & 2)));
   }
   flag[i] = h;
 }
@@ -202,14 +212,14 @@ __global__ void k_new_off(const uint32_t* __restrict__ start, uint64_t T, uint64
 
 // (lowTraceId, traceId) group heads over u (span indexes into v, grouped, ascending inside)
 __global__ void k_group_heads(const uint64_t* __restrict__ lo, const uint64_t* __restrict__ hi,
-                              const uint32_t* __restrict__ v, const uint32_t* __restrict__ u, uint64_t m,
-                              uint32_t* __restrict__ out) {
+                              const uint8_t* __restrict__ alive, const uint32_t* __restrict__ v,
+                              const uint32_t* __restrict__ u, uint64_t m, uint32_t* __restrict__ out) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= m) return;
   bool h = i == 0;
   if (!h) {
     const uint32_t a = v[u[i - 1]], b = v[u[i]];
-    h = lo[a] != lo[b] || hi[a] != hi[b];
+    h = lo[a] != lo[b] || hi[a] != hi[b] || ((alive[a] ^ alive[b]) & 2);
   }
   out[i] = h ? (uint32_t)i : 0u;
 }
@@ -301,9 +311,9 @@ hipError_t sort64(IndexWork& w, const uint64_t* kin, uint64_t* kout, const uint3
 }
 
 hipError_t sort32(IndexWork& w, const uint32_t* kin, uint32_t* kout, const uint32_t* vin, uint32_t* vout,
-                  uint64_t m, hipStream_t s) {
-  return cub_at(w, s, __LINE__, [&](void* t, size_t& b) {
-    return hipcub::DeviceRadixSort::SortPairs(t, b, kin, kout, vin, vout, (int)m, 0, 32, s);
+                  uint64_t m, hipStream_t s, int end_bit = 32) {
+  return cub_at(w, s, __LINE__ * 64 + end_bit, [&](void* t, size_t& b) {
+    return hipcub::DeviceRadixSort::SortPairs(t, b, kin, kout, vin, vout, (int)m, 0, end_bit, s);
   });
 }
 
@@ -495,18 +505,22 @@ hipError_t index_select(IndexWork& w, const uint64_t* lo, const uint64_t* hi, co
     LAUNCH(k_place, m, stored, w.u[0], w.seg, w.sv[0], w.u[1], m, perm);
     LAUNCH(k_new_off, T + 1, w.u[1], T, m, off);
   } else if (mode == SEL_ALL_STRICT) {
-    // group by (low id, trace id), indexes into `stored` ascending inside; a group goes where
-    // its first span is (first-seen order inside the low id)
-    LAUNCH(k_iota32, m, w.u[0], m);
-    LAUNCH(k_take, m, hi, stored, 0ull, w.k[0], m);
+    // group by (low id, trace id) - the normalized id string: its high 64 bits and its width,
+    // since a 17-31 digit id padded to 32 characters keeps a zero high half - indexes into
+    // `stored` ascending inside; a group goes where its first span is (first-seen order inside
+    // the low id)
+    LAUNCH(k_iota32, m, w.u[1], m);
+    LAUNCH(k_wide_key, m, alive, stored, w.u[2], m);
+    ITRY(sort32(w, w.u[2], w.u[3], w.u[1], w.u[0], m, s, 1));
+    LAUNCH(k_take2, m, hi, stored, w.u[0], w.k[0], m);
     ITRY(sort64(w, w.k[0], w.k[1], w.u[0], w.u[1], m, s));
     LAUNCH(k_take2, m, lo, stored, w.u[1], w.k[0], m);
     ITRY(sort64(w, w.k[0], w.k[1], w.u[1], w.u[0], m, s));
-    LAUNCH(k_group_heads, m, lo, hi, stored, w.u[0], m, w.u[2]);
+    LAUNCH(k_group_heads, m, lo, hi, alive, stored, w.u[0], m, w.u[2]);
     ITRY(max_scan(w, w.u[2], w.u[1], m, s));
     LAUNCH(k_group_first, m, w.u[0], w.u[1], m, w.u[2]);
     ITRY(sort32(w, w.u[2], w.u[1], stored, perm, m, s));
-    LAUNCH(k_trace_heads, m, lo, hi, perm, m, w.flag);
+    LAUNCH(k_trace_heads, m, lo, hi, alive, perm, m, w.flag);
     ITRY(offsets_of(w, w.flag, m, off, &T, s));
   } else {
     return hipErrorInvalidValue;

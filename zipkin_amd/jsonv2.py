@@ -127,7 +127,7 @@ class JsonV2Decoder:
         n = int(out.n_spans)
         if n == 0:
             return DecodedBatch(0, None)
-        return DecodedBatch(n, out.dev, out.dev_trace_hi, self._dec)
+        return DecodedBatch(n, out.dev, out.dev_trace_hi, self._dec, out.dev_trace_wide)
 
     def decode_columns(self, data: bytes) -> Columns:
         """Host columns of one decoded batch, one span per trace (as ``accept`` packs them)."""

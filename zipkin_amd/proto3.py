@@ -31,6 +31,7 @@ class DecodedBatch:
     dev: Optional[N.SpanCols]
     dev_trace_hi: Optional[int] = None  # device pointer: the trace ids' high 64 bits (0 = 64-bit id)
     _dec: Optional[N.Decoder] = None
+    dev_trace_wide: Optional[int] = None  # device pointer: the ids' widths (None: 128-bit iff hi != 0)
 
     def _host(self, name, dtype):
         if self.n_spans == 0:
@@ -72,7 +73,7 @@ class Proto3Decoder:
         n = int(out.n_spans)
         if n == 0:
             return DecodedBatch(0, None)
-        return DecodedBatch(n, out.dev, out.dev_trace_hi, self._dec)
+        return DecodedBatch(n, out.dev, out.dev_trace_hi, self._dec, out.dev_trace_wide)
 
     def decode_columns(self, data: bytes) -> Columns:
         """Host columns of one decoded batch, one span per trace (as ``accept`` packs them)."""

@@ -118,8 +118,11 @@ class InMemoryStorage:
             self._evict(len(spans))
             # one "trace" per span: grouping happens at query time
             cols = pack_traces([[s] for s in spans], self._linker.svc, self._linker.ip4, self._linker.ip6)
+            # the normalized id's high half and width (a 17-31 digit id pads to 32 characters, high
+            # half zero: strictByTraceId still tells it from the 16-character id)
             hi = np.array([int(s.trace_id[:16], 16) if len(s.trace_id) == 32 else 0 for s in spans], np.uint64)
-            self._st().append(cols, hi)
+            wide = np.array([len(s.trace_id) == 32 for s in spans], np.uint8)
+            self._st().append(cols, hi, wide)
         return Call(lambda: None)
 
     def accept_proto3(self, data: bytes) -> Call[None]:
@@ -134,7 +137,7 @@ class InMemoryStorage:
         b = self._decoder.decode(data)
         if b.n_spans:
             self._evict(b.n_spans)
-            self._st().append_device(b.dev, b.n_spans, b.dev_trace_hi)
+            self._st().append_device(b.dev, b.n_spans, b.dev_trace_hi, b.dev_trace_wide)
         return Call(lambda: None)
 
     acceptProto3 = accept_proto3
@@ -150,7 +153,7 @@ class InMemoryStorage:
         b = self._json_decoder.decode(data)
         if b.n_spans:
             self._evict(b.n_spans)
-            self._st().append_device(b.dev, b.n_spans, b.dev_trace_hi)
+            self._st().append_device(b.dev, b.n_spans, b.dev_trace_hi, b.dev_trace_wide)
         return Call(lambda: None)
 
     acceptJsonV2 = accept_json_v2
