@@ -695,7 +695,9 @@ def _read_span(r: _Reader) -> Span:
         key = r.next_name()
         if key == "traceId":  # Span.Builder.traceId -> normalizeTraceId (Span.java:402-405, 634-649)
             try:
-                trace_id = normalize_trace_id(r.next_string())
+                trace_id = r.next_string()
+                normalize_trace_id(trace_id)  # its errors here; Span.create normalizes it once, as the
+                # Builder does (normalizing twice would drop the zero high half a 17-31 digit id pads to)
             except ValueError as ex:
                 raise IllegalArgument(str(ex))
             continue

@@ -491,8 +491,13 @@ def test_gpu_numbers_through_parse_double():
             except J.IllegalArgument:
                 with pytest.raises(N.ReferenceIllegalArgumentException):
                     dec.decode_columns(data)
+                    pytest.fail(f"device accepts {data!r}")
                 continue
-            assert_same(dec.decode_columns(data), exp)
+            try:
+                got = dec.decode_columns(data)
+            except N.ZdlError as ex:
+                pytest.fail(f"device rejects {data!r}: {ex}")
+            assert_same(got, exp)
             n_ok += 1
     assert n_ok > 300
     dec.close()

@@ -375,7 +375,9 @@ hipError_t index_alive(IndexWork& w, const uint8_t* alive, uint64_t n, uint32_t*
   *m = 0;
   if (n == 0) return hipSuccess;
   ITRY(cub_at(w, s, __LINE__, [&](void* t, size_t& b) {
-    return hipcub::DeviceSelect::Flagged(t, b, hipcub::CountingInputIterator<uint32_t>(0), alive, out, w.d, (int)n, s);
+    // a predicate, not Flagged: the alive byte also carries the id-width bit (value 3), and the
+    // flags of a flagged select may be summed as integers
+    return hipcub::DeviceSelect::If(t, b, hipcub::CountingInputIterator<uint32_t>(0), out, w.d, (int)n, AliveOf{alive}, s);
   }));
   ITRY(fetch(w, 1, s));
   *m = w.h[0];
