@@ -177,6 +177,10 @@ const char* zdl_create_error(void);
 void        zdl_destroy(zdl_ctx* ctx);
 const char* zdl_last_error(const zdl_ctx* ctx);
 int         zdl_abi_version(void);
+/* Diagnostic: workgroups of the production k_link (table mode 0 hash, 1 dense, 2 LOG, 3 sorted
+ * log; window 0/1) resident per CU on `device` (the design needs 2: 80 KB of LDS each); -1 on
+ * error. */
+int         zdl_link_occupancy(int device, int table_mode, int window);
 
 /* rank[id] = position of dictionary string `id` in java.lang.String order. Without a
  * table the id itself is the rank. n must cover every id the columns use. */

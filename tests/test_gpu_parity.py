@@ -296,3 +296,13 @@ def test_ungrouped_input_grouped_on_device(use_ord):
             np.repeat(np.arange(cols.n_traces), np.diff(cols.offsets.astype(np.int64))), rng)))
     assert _sorted_links(ctx) == exp
     ctx.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tm,window", [(1, 0), (1, 1), (2, 0), (2, 1), (3, 0), (0, 0)])
+def test_k_link_two_workgroups_per_cu(tm, window):
+    """k_link's design point: two 16-wave workgroups per CU (8 waves a SIMD), each with exactly
+    80 KB of LDS in the dense mode. A few bytes of static __shared__ in k_link (or in anything it
+    calls) halve that silently - it cost C2's k_link 127 -> 165 us once (profiles/r03f_*)."""
+    from zipkin_amd import _native as N
+    assert N.lib().zdl_link_occupancy(0, tm, window) == 2

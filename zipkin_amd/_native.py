@@ -37,7 +37,7 @@ PF_RPORT = 1 << 24
 KIND_NULL = 7
 
 EXPORTS = (
-    "zdl_abi_version", "zdl_create", "zdl_create_error", "zdl_destroy", "zdl_last_error",
+    "zdl_abi_version", "zdl_link_occupancy", "zdl_create", "zdl_create_error", "zdl_destroy", "zdl_last_error",
     "zdl_set_ranks", "zdl_set_window", "zdl_put_spans", "zdl_put_spans_device", "zdl_sync",
     "zdl_link", "zdl_merge_links", "zdl_add_links", "zdl_reset", "zdl_table_export",
     "zdl_table_import", "zdl_get_kernel_times", "zdl_stream", "zdl_set_days", "zdl_link_days",
@@ -128,6 +128,8 @@ def lib() -> C.CDLL:
     L = C.CDLL(LIB_PATH)
     vp, i32, u32, u64, i64 = C.c_void_p, C.c_int32, C.c_uint32, C.c_uint64, C.c_int64
     L.zdl_abi_version.restype = C.c_int
+    L.zdl_link_occupancy.restype = C.c_int
+    L.zdl_link_occupancy.argtypes = [C.c_int, C.c_int, C.c_int]
     L.zdl_create.restype = vp
     L.zdl_create.argtypes = [C.POINTER(Config)]
     L.zdl_create_error.restype = C.c_char_p

@@ -173,14 +173,17 @@ struct Args {
   const uint8_t* gstat;
   const uint32_t* grest;    // and then the back-list indexes k_tail links instead of the whole back
   const uint32_t* grest_n;  // list (the giant ones dropped; the ones the tier rejected appended)
+  uint8_t* bstat;           // k_big's verdict per back-list index (1 linked, 2 exact path), or null
+  uint32_t* tick_big;       // k_big's trace tickets
 };
 // The counter block of one put (two alternate by put, so no put issues a memset)
-enum : int { CTR_MID = 0, CTR_CX = 1, CTR_LARGE = 2, CTR_TICK_LARGE = 3, CTR_TICK_MID = 4, CTR_RETRY = 5, CTR_N = 8 };
+enum : int { CTR_MID = 0, CTR_CX = 1, CTR_LARGE = 2, CTR_TICK_LARGE = 3, CTR_TICK_MID = 4, CTR_RETRY = 5,
+             CTR_TICK_BIG = 6, CTR_N = 8 };
 constexpr int CTR_DONE = 2 * CTR_N;  // k_tail's finished-workgroup count (after both blocks)
 
 #include "zdl_full.inc"  // the full per-window emulation (k_tail's first part)
 constexpr unsigned long long FLAG_TAIL = 1ull << 62;  // lazy put: k_mid / k_tail still have work
-__device__ void lk_lazy_end(const Args& A);          // k_link's end in a lazy put (below)
+__device__ void lk_lazy_end(const Args& A, uint32_t* scratch);  // k_link's end in a lazy put (below)
 #include "zdl_link.inc"  // k_link, full_windows (need zdl_full.inc's helpers)
 #include "zdl_log.inc"   // LOG mode reduce: k_pscan, k_scatter, k_hist
 
@@ -1023,11 +1026,13 @@ __device__ __forceinline__ void big_exact(const Args& A, uint64_t b, int n, uint
 
 // One big trace with the workgroup (every thread calls): the time-window / day filters, then
 // big_simple, else (or with try_simple false) the exact path.
-template <int ORD>
-__device__ __forceinline__ void big_one(const Args& A, unsigned char* lds, size_t lds_bytes, uint32_t bi, bool try_simple) {
+// SIMPLE_ONLY (k_big): no exact path; returns false when the trace needs it (not simple).
+template <int ORD, bool SIMPLE_ONLY = false>
+__device__ __forceinline__ bool big_one(const Args& A, unsigned char* lds, size_t lds_bytes, uint32_t bi, bool try_simple) {
   __shared__ uint32_t sh_cnt;  // sparse: links logged for the current trace (big_simple)
   __shared__ int sh_act;
   __shared__ int64_t sh_ts_root_idx, sh_ts_min;
+  bool handled = true;
   do {
     const uint32_t t = A.big_list[bi];
     const uint64_t b = A.off[t];
@@ -1109,9 +1114,11 @@ __device__ __forceinline__ void big_one(const Args& A, unsigned char* lds, size_
       if (A.sparse && threadIdx.x == 0) A.tseg_big[bi] = sh_cnt;
       continue;
     }
-    big_exact<ORD>(A, b, n, day, bi);
+    if (SIMPLE_ONLY) handled = false;
+    else big_exact<ORD>(A, b, n, day, bi);
   } while (false);
   big_sync();
+  return handled;
 }
 
 #include "zdl_giant.inc"  // the device-wide tier for big traces (sparse contexts)
@@ -1149,13 +1156,13 @@ __device__ __forceinline__ unsigned long long ld_agent(const unsigned long long*
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// wsum: COMPACT_WG / 64 + 1 words of LDS scratch.
 __device__ __forceinline__ void compact_ordered(const unsigned long long* __restrict__ call,
                                                 const unsigned long long* __restrict__ err, uint32_t SS,
                                                 uint32_t S, const uint32_t* __restrict__ status,
-                                                unsigned long long* __restrict__ meta) {
+                                                unsigned long long* __restrict__ meta, uint32_t* wsum) {
   constexpr int KMAX = 8;  // cells per thread: SS <= COMPACT_WG * KMAX
   const MapCols out = map_cols(meta);
-  __shared__ uint32_t wsum[COMPACT_WG / 64 + 1];
   const uint32_t K = (SS + COMPACT_WG - 1) / COMPACT_WG, c0 = threadIdx.x * K;
   unsigned long long cv[KMAX];
   uint32_t nz = 0;
@@ -1205,8 +1212,11 @@ __device__ __forceinline__ void compact_ordered(const unsigned long long* __rest
 // queued window) it compacts the table into the mapped buffer, zeroes the next put's counter
 // slots and releases `seq` - the put is complete without launching them; otherwise it stores
 // seq | FLAG_TAIL and the host launches them (zdl_link, or the context's next call).
-__device__ void lk_lazy_end(const Args& A) {
-  __shared__ bool last, tail;
+__device__ void lk_lazy_end(const Args& A, uint32_t* scratch) {
+  // scratch (LDS, after the table flush): [0] last, [1] tail, [4..] compact_ordered's sums
+  uint32_t& last = scratch[0];
+  uint32_t& tail = scratch[1];
+  __syncthreads();  // every wave is past its flush's LDS reads
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0)
@@ -1220,7 +1230,7 @@ __device__ void lk_lazy_end(const Args& A) {
     tail = (b | l | x) != 0;
   }
   __syncthreads();
-  if (!tail) compact_ordered(A.call, A.err, A.rows * A.S, A.S, A.status, A.map);
+  if (!tail) compact_ordered(A.call, A.err, A.rows * A.S, A.S, A.status, A.map, scratch + 4);
   __syncthreads();
   if (!tail && threadIdx.x < CTR_N) A.ctr_next[threadIdx.x] = 0;  // k_tail's job when it runs
   if (threadIdx.x == 0) {
@@ -1235,7 +1245,8 @@ __global__ void __launch_bounds__(COMPACT_WG) k_compact_ordered(const unsigned l
                                                                 uint32_t SS, uint32_t S,
                                                                 const uint32_t* __restrict__ status,
                                                                 unsigned long long* __restrict__ meta) {
-  compact_ordered(call, err, SS, S, status, meta);
+  __shared__ uint32_t wsum[COMPACT_WG / 64 + 1];
+  compact_ordered(call, err, SS, S, status, meta, wsum);
 }
 
 // ------------------------------------------------------------------- k_tail
@@ -1274,7 +1285,8 @@ __global__ void __launch_bounds__(TAIL_WG, 1) k_tail(Args A) {
       if (threadIdx.x == 0) sh_j = atomicAdd(A.tick_large, 1u);
       const bool back = j < nlarge;
       const uint32_t bi = back ? (A.grest ? A.grest[j] : A.big_cap - 1u - j) : A.retry[j - nlarge];
-      const uint8_t gs = back && A.gstat ? A.gstat[bi] : 0;  // the giant tier's verdict (uniform)
+      // k_big's verdict (or the giant tier's when k_big did not run): 1 linked, 2 the exact path
+      const uint8_t gs = !back ? 0 : A.bstat ? A.bstat[bi] : A.gstat ? A.gstat[bi] : 0;  // (uniform)
       if (gs != 1) big_one<ORD>(A, lds, tail_block_bytes(WINDOW), bi, back && gs == 0);
     }
   }
@@ -1292,12 +1304,40 @@ __global__ void __launch_bounds__(TAIL_WG, 1) k_tail(Args A) {
     last = __hip_atomic_fetch_add(A.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   __syncthreads();
   if (!last) return;
-  compact_ordered(A.call, A.err, A.rows * A.S, A.S, A.status, A.map);
+  __shared__ uint32_t wsum[COMPACT_WG / 64 + 1];
+  compact_ordered(A.call, A.err, A.rows * A.S, A.S, A.status, A.map, wsum);
   __syncthreads();
   if (threadIdx.x == 0) {
     *A.done = 0;
     __threadfence_system();  // the records and counts are visible to the host before the flag
     __hip_atomic_store(A.flag, A.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// k_big: the back list's big traces by big_simple alone (the time-window / day filters
+// included), one workgroup each by ticket, before k_tail; what is not simple is left to
+// k_tail's exact path. Its own kernel so that big_simple's registers never meet
+// full_windows' and big_exact's: together they spilled k_tail at 1024 threads (52 VGPRs, 244 B
+// of scratch per lane: 1.9 GB of scratch writes per C5 put, profiles/r03e_hbm_c2_c5.json).
+// bstat[bi] = 1 linked (or outside the window), 2 for k_tail's exact path.
+__global__ void __launch_bounds__(TAIL_WG, 1) k_big(Args A) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  __shared__ uint32_t sh_j;
+  const uint32_t nlarge = A.grest ? *A.grest_n : *A.large_count;
+  if (nlarge == 0) return;
+  const size_t lds_bytes = tail_block_bytes(A.days ? 2 : A.window);
+  if (threadIdx.x == 0) sh_j = atomicAdd(A.tick_big, 1u);
+  while (true) {
+    __syncthreads();
+    const uint32_t j = sh_j;
+    __syncthreads();
+    if (j >= nlarge) break;
+    if (threadIdx.x == 0) sh_j = atomicAdd(A.tick_big, 1u);
+    const uint32_t bi = A.grest ? A.grest[j] : A.big_cap - 1u - j;
+    const uint8_t gs = A.gstat ? A.gstat[bi] : 0;  // the giant tier's verdict (uniform)
+    uint8_t st = gs;
+    if (gs == 0) st = big_one<0, true>(A, lds, lds_bytes, bi, true) ? 1 : 2;
+    if (threadIdx.x == 0) A.bstat[bi] = st;
   }
 }
 
@@ -1420,7 +1460,8 @@ struct zdl_ctx {
   uint64_t span_base = 0;
   DevBuf<uint32_t> o_fa, o_fb, o_bfs;
   // per-put scratch
-  DevBuf<uint32_t> big_list, counters;  // counters: two CTR_N blocks alternating by put, then done
+  DevBuf<uint32_t> big_list, counters;
+  DevBuf<uint8_t> big_stat;  // k_big's verdicts  // counters: two CTR_N blocks alternating by put, then done
   DevBuf<uint32_t> retry;  // k_tail: wave_big traces for the exact path
   uint32_t epoch = 0;
   DevBuf<uint64_t> cx_win;
@@ -1507,6 +1548,10 @@ struct zdl_ctx {
   unsigned char* h_rec = nullptr;
   unsigned char* d_rec = nullptr;
   size_t h_rec_cap = 0;
+  // ... staged in HBM first (same column layout) and copied by the DMA engine: a compaction
+  // kernel storing over PCIe held its CUs for the whole transfer (1.9 ms at C5), so the other
+  // step in flight could not run beside it
+  DevBuf<unsigned char> rec_dev;
   DevBuf<uint64_t> o_first;
   DevBuf<int32_t> mi_p, mi_c;
   DevBuf<int64_t> mi_call, mi_err;
@@ -1641,6 +1686,20 @@ extern "C" {
 
 int zdl_abi_version(void) { return ZDL_ABI_VERSION; }
 
+int zdl_link_occupancy(int device, int table_mode, int window) {
+  if (table_mode < TM_HASH || table_mode > TM_SORT || window < 0 || window > 1) return -1;
+  if (hipSetDevice(device) != hipSuccess) return -1;
+  const void* f = k_link_fn(table_mode, window);
+  if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)link_block_bytes(window, table_mode)) !=
+      hipSuccess)
+    return -1;
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, lk::waves(window) * 64, link_block_bytes(window, table_mode)) !=
+      hipSuccess)
+    return -1;
+  return n;
+}
+
 const char* zdl_create_error(void) { return g_create_error.c_str(); }
 
 static zdl_ctx* create_group(const zdl_config* cfg);
@@ -1713,6 +1772,9 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
   }
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)k_g_join, hipFuncAttributeMaxDynamicSharedMemorySize, GHCAP * 16);
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)k_big, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)std::max(tail_block_bytes(0), std::max(tail_block_bytes(1), tail_block_bytes(2))));
   for (int d = 0; d < 2 && e == hipSuccess; ++d)
     for (int w = 0; w < 3 && e == hipSuccess; ++w)
       for (int o = 0; o < 2 && e == hipSuccess; ++o)
@@ -1769,7 +1831,7 @@ void zdl_destroy(zdl_ctx* c) {
   for (auto& r : c->rank) r.release();
   c->call.release(); c->errc.release(); c->status.release();
   c->first.release(); c->day_first.release(); c->o_key.release(); c->o_fa.release(); c->o_fb.release(); c->o_bfs.release();
-  c->big_list.release(); c->counters.release(); c->retry.release();
+  c->big_list.release(); c->big_stat.release(); c->counters.release(); c->retry.release();
   c->cx_win.release();
   if (c->prof_on && c->prof.p) {
     unsigned long long h[12] = {};
@@ -1834,6 +1896,7 @@ void zdl_destroy(zdl_ctx* c) {
   if (c->h_map) (void)hipHostFree(c->h_map);
   if (c->h_flag) (void)hipHostFree(c->h_flag);
   if (c->h_rec) (void)hipHostFree(c->h_rec);
+  c->rec_dev.release();
   c->mi_p.release(); c->mi_c.release(); c->mi_call.release(); c->mi_err.release();
   for (auto& ev : c->ev)
     if (ev) (void)hipEventDestroy(ev);
@@ -2138,6 +2201,14 @@ static int resolve_lazy(zdl_ctx* c, bool wait) {
       return hip_fail(c, me, "k_mid launch");
     }
   }
+  if (A.bstat) {
+    const hipError_t be = hipLaunchKernel((const void*)k_big, dim3(c->grid), dim3(TAIL_WG), kargs,
+                                          tail_block_bytes(c->lazy_wmode), c->stream);
+    if (be != hipSuccess) {
+      c->poisoned = true;
+      return hip_fail(c, be, "k_big launch");
+    }
+  }
   const hipError_t le = hipLaunchKernel(k_tail_fn(c->lazy_dense, c->lazy_wmode, 0), dim3(c->grid), dim3(TAIL_WG), kargs,
                                         tail_block_bytes(c->lazy_wmode), c->stream);
   if (le != hipSuccess) {
@@ -2174,6 +2245,7 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   }
   const int grid = c->grid, lgrid = c->cus * lk::wgs_per_cu;  // k_link: two 16-wave workgroups per CU
   HIP_TRY(c, c->big_list.ensure(n_traces));
+  HIP_TRY(c, c->big_stat.ensure(n_traces));
   // queued windows: at most one per trace; mode 3 (insertion order) uses one slot per trace
   HIP_TRY(c, c->cx_win.ensure(2 * ((c->ord || c->days) ? n_traces : std::min<uint64_t>(n_traces, n_spans))));
   Args A{};
@@ -2198,6 +2270,7 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   A.call = c->call.p;
   A.err = c->errc.p;
   A.big_list = c->big_list.p;
+  A.bstat = c->ord ? nullptr : c->big_stat.p;  // k_big runs (insertion order: every big trace exact)
   const uint32_t ep = c->epoch & 1u;
   uint32_t* ctr = c->counters.p + ep * CTR_N;
   A.big_count = ctr + CTR_MID;
@@ -2205,6 +2278,7 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   A.tick_large = ctr + CTR_TICK_LARGE;
   A.tick_mid = ctr + CTR_TICK_MID;
   A.retry_count = ctr + CTR_RETRY;
+  A.tick_big = ctr + CTR_TICK_BIG;
   A.ctr_next = c->counters.p + (ep ^ 1u) * CTR_N;
   A.big_cap = (uint32_t)n_traces;
   A.status = c->status.p;
@@ -2384,6 +2458,14 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
     }
   }
   ev_record(c, 8);
+  if (A.bstat) {
+    const hipError_t be = hipLaunchKernel((const void*)k_big, dim3(grid), dim3(TAIL_WG), kargs, tail_block_bytes(wmode),
+                                          c->stream);
+    if (be != hipSuccess) {
+      c->poisoned = true;
+      return hip_fail(c, be, "k_big launch");
+    }
+  }
   const hipError_t le = hipLaunchKernel(k_tail_fn(c->sparse ? 2 : dense, wmode, c->ord ? 1 : 0), dim3(grid),
                                         dim3(TAIL_WG), kargs, tail_block_bytes(wmode), c->stream);
   if (le != hipSuccess) {
@@ -3016,6 +3098,7 @@ static int link_insertion(zdl_ctx* c, zdl_links* out) {
 
 }  // extern "C"
 
+static int rec_download(zdl_ctx* c, uint64_t m);
 static int ensure_rec(zdl_ctx* c, uint64_t m);
 
 // zdl_link's sorted output from the S x S tables (call, err) on c's device: c's own tables
@@ -3073,10 +3156,13 @@ static int link_sorted(zdl_ctx* c, const unsigned long long* call, const unsigne
     const int erc = ensure_rec(c, m);
     if (erc != ZDL_OK) return erc;
     const size_t cap = c->h_rec_cap;
+    unsigned char* const d = c->rec_dev.p;
     HIP_TRY(c, compact_records(c->lw, call, err, m, c->S, c->nrank[0] ? c->rank[0].p : nullptr, c->nrank[0],
-                               (int32_t*)c->d_rec, (int32_t*)(c->d_rec + 4 * cap), (int64_t*)(c->d_rec + 8 * cap),
-                               (int64_t*)(c->d_rec + 16 * cap), c->stream));
+                               (int32_t*)d, (int32_t*)(d + 4 * cap), (int64_t*)(d + 8 * cap),
+                               (int64_t*)(d + 16 * cap), c->stream));
     ev_record(c, 6);
+    const int drc = rec_download(c, m);
+    if (drc != ZDL_OK) return drc;
     HIP_TRY(c, hipMemcpyAsync(c->h_meta, c->status.p, 16, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     put_times(c);
@@ -3102,9 +3188,11 @@ static int link_sorted(zdl_ctx* c, const unsigned long long* call, const unsigne
 
 static int comm_sum_tables(zdl_ctx* c);  // multi-process job: every rank's tables summed (below)
 
-// The mapped pinned output columns (parent, child i32; call, err i64) for m links.
+// The mapped pinned output columns (parent, child i32; call, err i64) for m links, and their
+// HBM staging copy.
 static int ensure_rec(zdl_ctx* c, uint64_t m) {
   if (m <= c->h_rec_cap) return ZDL_OK;
+  c->rec_dev.release();
   if (c->h_rec) (void)hipHostFree(c->h_rec);
   c->h_rec = nullptr;
   c->d_rec = nullptr;
@@ -3112,7 +3200,19 @@ static int ensure_rec(zdl_ctx* c, uint64_t m) {
   const size_t cap = std::max<size_t>((size_t)(m + m / 2 + 1) & ~(size_t)1, 1024);
   HIP_TRY(c, hipHostMalloc((void**)&c->h_rec, cap * 24, hipHostMallocMapped | hipHostMallocCoherent));
   HIP_TRY(c, hipHostGetDevicePointer((void**)&c->d_rec, c->h_rec, 0));
+  HIP_TRY(c, c->rec_dev.ensure(cap * 24));
   c->h_rec_cap = cap;
+  return ZDL_OK;
+}
+
+// The first m records of each staged column to the pinned host columns (DMA, on the stream).
+static int rec_download(zdl_ctx* c, uint64_t m) {
+  const size_t cap = c->h_rec_cap;
+  if (m == 0) return ZDL_OK;
+  for (size_t off : {(size_t)0, 4 * cap})
+    HIP_TRY(c, hipMemcpyAsync(c->h_rec + off, c->rec_dev.p + off, m * 4, hipMemcpyDeviceToHost, c->stream));
+  for (size_t off : {8 * cap, 16 * cap})
+    HIP_TRY(c, hipMemcpyAsync(c->h_rec + off, c->rec_dev.p + off, m * 8, hipMemcpyDeviceToHost, c->stream));
   return ZDL_OK;
 }
 
@@ -3125,11 +3225,14 @@ static int link_sparse_start(zdl_ctx* c, const SparseTable& t) {
   if (rc != ZDL_OK) return rc;
   const size_t cap = c->h_rec_cap;
   ev_record(c, 5);
+  unsigned char* const d = c->rec_dev.p;
   HIP_TRY(c, compact_sparse(c->lw, t.cell, t.call, t.err, m, c->S,
-                            c->nrank[0] ? c->rank[0].p : nullptr, c->nrank[0], (int32_t*)c->d_rec,
-                            (int32_t*)(c->d_rec + 4 * cap), (int64_t*)(c->d_rec + 8 * cap),
-                            (int64_t*)(c->d_rec + 16 * cap), c->stream));
+                            c->nrank[0] ? c->rank[0].p : nullptr, c->nrank[0], (int32_t*)d,
+                            (int32_t*)(d + 4 * cap), (int64_t*)(d + 8 * cap),
+                            (int64_t*)(d + 16 * cap), c->stream));
   ev_record(c, 6);
+  rc = rec_download(c, m);
+  if (rc != ZDL_OK) return rc;
   HIP_TRY(c, hipMemcpyAsync(c->h_meta, c->status.p, 16, hipMemcpyDeviceToHost, c->stream));
   return ZDL_OK;
 }
