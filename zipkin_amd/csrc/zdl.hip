@@ -3188,6 +3188,24 @@ static int link_sorted(zdl_ctx* c, const unsigned long long* call, const unsigne
 
 static int comm_sum_tables(zdl_ctx* c);  // multi-process job: every rank's tables summed (below)
 
+// Four byte ranges [off, off + len) copied from HBM to mapped pinned host memory (same offsets
+// on both sides; offsets multiples of 8, lengths multiples of 4), 8 bytes a lane, grid-stride.
+struct PcieSegs {
+  size_t off[4], len[4];
+};
+__global__ void __launch_bounds__(256) k_pcie_copy(unsigned char* __restrict__ dst, const unsigned char* __restrict__ src,
+                                                   PcieSegs g) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x, T = (size_t)gridDim.x * blockDim.x;
+  for (int k = 0; k < 4; ++k) {
+    const size_t n8 = g.len[k] / 8;
+    const uint64_t* s = reinterpret_cast<const uint64_t*>(src + g.off[k]);
+    uint64_t* d = reinterpret_cast<uint64_t*>(dst + g.off[k]);
+    for (size_t i = t; i < n8; i += T) __builtin_nontemporal_store(s[i], d + i);
+    if (t == 0 && (g.len[k] & 7))
+      *reinterpret_cast<uint32_t*>(dst + g.off[k] + 8 * n8) = *reinterpret_cast<const uint32_t*>(src + g.off[k] + 8 * n8);
+  }
+}
+
 // The mapped pinned output columns (parent, child i32; call, err i64) for m links, and their
 // HBM staging copy.
 static int ensure_rec(zdl_ctx* c, uint64_t m) {
@@ -3205,14 +3223,25 @@ static int ensure_rec(zdl_ctx* c, uint64_t m) {
   return ZDL_OK;
 }
 
-// The first m records of each staged column to the pinned host columns (DMA, on the stream).
+// The first m records of each staged column to the pinned host columns, by a narrow copy kernel
+// (k_pcie_copy: PCIe-bound at any width, so it leaves the other CUs to the next put's kernels;
+// hipMemcpyAsync ran rocclr's copyBuffer blit kernels across the whole GPU and slowed the
+// concurrent k_link from 0.66 to 2.1 ms, profiles/r03g_c5_timeline.txt).
 static int rec_download(zdl_ctx* c, uint64_t m) {
   const size_t cap = c->h_rec_cap;
   if (m == 0) return ZDL_OK;
-  for (size_t off : {(size_t)0, 4 * cap})
-    HIP_TRY(c, hipMemcpyAsync(c->h_rec + off, c->rec_dev.p + off, m * 4, hipMemcpyDeviceToHost, c->stream));
-  for (size_t off : {8 * cap, 16 * cap})
-    HIP_TRY(c, hipMemcpyAsync(c->h_rec + off, c->rec_dev.p + off, m * 8, hipMemcpyDeviceToHost, c->stream));
+  static const int wgs = [] {
+    const char* e = getenv("ZDL_PCIE_WGS");
+    return e ? std::max(1, atoi(e)) : 8;  // 8 / 32 / 64: C5 two in flight 6.73 / 7.08 / 7.17 ms
+  }();
+  PcieSegs g{};
+  const size_t off[4] = {0, 4 * cap, 8 * cap, 16 * cap}, len[4] = {4 * m, 4 * m, 8 * m, 8 * m};
+  for (int k = 0; k < 4; ++k) {
+    g.off[k] = off[k];
+    g.len[k] = len[k];
+  }
+  hipLaunchKernelGGL(k_pcie_copy, dim3((unsigned)wgs), dim3(256), 0, c->stream, c->d_rec, c->rec_dev.p, g);
+  HIP_TRY(c, hipGetLastError());
   return ZDL_OK;
 }
 
