@@ -175,10 +175,11 @@ struct Args {
   const uint32_t* grest_n;  // list (the giant ones dropped; the ones the tier rejected appended)
   uint8_t* bstat;           // k_big's verdict per back-list index (1 linked, 2 exact path), or null
   uint32_t* tick_big;       // k_big's trace tickets
+  uint32_t kb_small;        // k_big<256> takes the traces of at most this many spans (<= KB_SMALL)
 };
 // The counter block of one put (two alternate by put, so no put issues a memset)
 enum : int { CTR_MID = 0, CTR_CX = 1, CTR_LARGE = 2, CTR_TICK_LARGE = 3, CTR_TICK_MID = 4, CTR_RETRY = 5,
-             CTR_TICK_BIG = 6, CTR_N = 8 };
+             CTR_TICK_BIG = 6, CTR_N = 8 };  // (CTR_TICK_BIG + 1: k_big<256>'s tickets)
 constexpr int CTR_DONE = 2 * CTR_N;  // k_tail's finished-workgroup count (after both blocks)
 
 #include "zdl_full.inc"  // the full per-window emulation (k_tail's first part)
@@ -363,9 +364,10 @@ __device__ __forceinline__ int bs_find(const BSView& v, uint64_t key, int n) {
   }
 }
 
+template <int NT = BIG_WG>  // threads of the workgroup
 __device__ __forceinline__ bool big_simple(const Args& A, unsigned char* lds, size_t lds_bytes, uint64_t b, int n, uint32_t day,
                            uint32_t* scnt) {
-  __shared__ int sh_bad, sh_more;
+  __shared__ int sh_bad, sh_more[3];
   __shared__ unsigned long long sh_rootid;
   __shared__ int sh_rp;
   BSView v;
@@ -407,12 +409,12 @@ __device__ __forceinline__ bool big_simple(const Args& A, unsigned char* lds, si
     sh_rootid = ~0ull;
     sh_rp = PAR_TERMINAL;
   }
-  for (int i = threadIdx.x; i < 2 * n; i += BIG_WG) {
+  for (int i = threadIdx.x; i < 2 * n; i += NT) {
     v.hk[i] = 0ull;
     v.hns[i] = 0u;
     v.hsh[i] = 0u;
   }
-  for (int i = threadIdx.x; i < n; i += BIG_WG) {
+  for (int i = threadIdx.x; i < n; i += NT) {
     const uint64_t g = b + i;
     const uint64_t id = A.c.id[g];
     const uint64_t pid = A.c.pid[g];
@@ -427,7 +429,7 @@ __device__ __forceinline__ bool big_simple(const Args& A, unsigned char* lds, si
   }
   __syncthreads();
   // 1. the id hash; a second span with one (id, shared) -> not simple
-  for (int i = threadIdx.x; i < n; i += BIG_WG) {
+  for (int i = threadIdx.x; i < n; i += NT) {
     const uint64_t id = v.id[i];
     int q = bs_slot(id, n);
     while (true) {
@@ -451,7 +453,7 @@ __device__ __forceinline__ bool big_simple(const Args& A, unsigned char* lds, si
   __syncthreads();
   const int rp = sh_rp, root_attach = rp >= 0 ? rp : PAR_TERMINAL;
   // 2. tree parents (+ the shared spans' parent-id backfill) and has-children
-  for (int i = threadIdx.x; i < n; i += BIG_WG) {
+  for (int i = threadIdx.x; i < n; i += NT) {
     const uint32_t pf = v.pf[i];
     int par;
     if (is_shared(pf)) {
@@ -485,13 +487,20 @@ __device__ __forceinline__ bool big_simple(const Args& A, unsigned char* lds, si
   }
   __syncthreads();
   // 3. pointer jumping: a -> PAR_TERMINAL iff reachable, nm -> nearest ancestor with a kind
+  // Round r's "anything moved" flag is sh_more[r % 3], cleared by thread 0 in round r - 1 before
+  // that round's barrier (so before any round-r writer) and after every reader of round r - 3
+  // has passed round r - 2's barrier. (One flag cleared at the top of each round let a fast
+  // wave clear it while a slow one had still to read the previous round's value: the slow
+  // wave left the loop early, the barriers paired up across phases and traces, and LDS was
+  // overwritten under it - garbage cells or a faulting access once four workgroups shared a CU.)
   int rounds = 4;
   for (int m = n; m > 1; m >>= 1) rounds += 2;
+  if (threadIdx.x == 0) sh_more[0] = 0;
+  __syncthreads();
   for (int r = 0; r < rounds; ++r) {
-    if (threadIdx.x == 0) sh_more = 0;
-    __syncthreads();
+    if (threadIdx.x == 0) sh_more[(r + 1) % 3] = 0;
     bool more = false;
-    for (int i = threadIdx.x; i < n; i += BIG_WG) {
+    for (int i = threadIdx.x; i < n; i += NT) {
       const int x = v.a[i];
       if (x >= 0) {
         v.a[i] = v.a[x];
@@ -503,18 +512,18 @@ __device__ __forceinline__ bool big_simple(const Args& A, unsigned char* lds, si
         more = true;
       }
     }
-    if (more) sh_more = 1;
+    if (more) sh_more[r % 3] = 1;
     __syncthreads();
-    if (!sh_more) break;
+    if (!sh_more[r % 3]) break;
   }
   if (A.tr_parent)
-    for (int i = threadIdx.x; i < n; i += BIG_WG) {
+    for (int i = threadIdx.x; i < n; i += NT) {
       const bool rch = v.a[i] == PAR_TERMINAL;
       A.tr_bfs[b + i] = rch ? 0 : -1;
       A.tr_anc[b + i] = rch && v.nm[i] >= 0 ? (int32_t)(b + v.nm[i]) : -1;
     }
   // 4. DependencyLinker's rules per node (every span of a simple trace is a node)
-  for (int i = threadIdx.x; i < n; i += BIG_WG) {
+  for (int i = threadIdx.x; i < n; i += NT) {
     if (v.a[i] != PAR_TERMINAL) continue;  // unreachable (a cycle not through the root)
     const uint32_t pf = v.pf[i];
     const uint32_t kind0 = kind_of(pf);
@@ -1027,7 +1036,7 @@ __device__ __forceinline__ void big_exact(const Args& A, uint64_t b, int n, uint
 // One big trace with the workgroup (every thread calls): the time-window / day filters, then
 // big_simple, else (or with try_simple false) the exact path.
 // SIMPLE_ONLY (k_big): no exact path; returns false when the trace needs it (not simple).
-template <int ORD, bool SIMPLE_ONLY = false>
+template <int ORD, bool SIMPLE_ONLY = false, int NT = BIG_WG>
 __device__ __forceinline__ bool big_one(const Args& A, unsigned char* lds, size_t lds_bytes, uint32_t bi, bool try_simple) {
   __shared__ uint32_t sh_cnt;  // sparse: links logged for the current trace (big_simple)
   __shared__ int sh_act;
@@ -1051,7 +1060,7 @@ __device__ __forceinline__ bool big_one(const Args& A, unsigned char* lds, size_
     big_sync();
     if (A.window) {
       // first parentless span with a timestamp (storage order), else the minimum one
-      for (int s = threadIdx.x; s < n; s += BIG_WG) {
+      for (int s = threadIdx.x; s < n; s += NT) {
         const int64_t x = A.c.ts[b + s];
         if (x == 0) continue;
         const uint64_t pid = A.c.pid[b + s];
@@ -1062,7 +1071,7 @@ __device__ __forceinline__ bool big_one(const Args& A, unsigned char* lds, size_
         sh_ts_min = A.c.ts[b + sh_ts_root_idx];
       big_sync();
       if (sh_ts_root_idx == 0x7fffffffffffffffll) {
-        for (int s = threadIdx.x; s < n; s += BIG_WG) {
+        for (int s = threadIdx.x; s < n; s += NT) {
           const int64_t x = A.c.ts[b + s];
           if (x != 0) {
             // atomicMin over positive micros; 0 stays "unset"
@@ -1084,7 +1093,7 @@ __device__ __forceinline__ bool big_one(const Args& A, unsigned char* lds, size_
     if (A.days) {  // daily buckets: flooredTraceTimestamp over the trace in storage order
       if (threadIdx.x == 0) sh_ts_root_idx = 0x7fffffffffffffffll;
       big_sync();
-      for (int s = threadIdx.x; s < n; s += BIG_WG)  // the first span with a timestamp
+      for (int s = threadIdx.x; s < n; s += NT)  // the first span with a timestamp
         if (A.c.ts[b + s] != 0) atomicMin((long long*)&sh_ts_root_idx, (long long)s);
       big_sync();
       const int f0 = sh_ts_root_idx == 0x7fffffffffffffffll ? n : (int)sh_ts_root_idx;
@@ -1092,7 +1101,7 @@ __device__ __forceinline__ bool big_one(const Args& A, unsigned char* lds, size_
       if (threadIdx.x == 0) sh_act = 0;
       big_sync();
       // a later span changes m only if its micros compare below m's millis: find any
-      for (int s = f0 + 1 + threadIdx.x; s < n; s += BIG_WG)
+      for (int s = f0 + 1 + threadIdx.x; s < n; s += NT)
         if (A.c.ts[b + s] != 0 && A.c.ts[b + s] < m1) sh_act = 1;
       big_sync();
       if (threadIdx.x == 0) {
@@ -1110,7 +1119,7 @@ __device__ __forceinline__ bool big_one(const Args& A, unsigned char* lds, size_
       if (sh_ts_min < 0) { big_sync(); continue; }
     }
     const uint32_t day = A.days ? (uint32_t)sh_ts_min : 0u;
-    if (!ORD && try_simple && !A.skip_simple && big_simple(A, lds, lds_bytes, b, n, day, &sh_cnt)) {
+    if (!ORD && try_simple && !A.skip_simple && big_simple<NT>(A, lds, lds_bytes, b, n, day, &sh_cnt)) {
       if (A.sparse && threadIdx.x == 0) A.tseg_big[bi] = sh_cnt;
       continue;
     }
@@ -1315,29 +1324,43 @@ __global__ void __launch_bounds__(TAIL_WG, 1) k_tail(Args A) {
 }
 
 // k_big: the back list's big traces by big_simple alone (the time-window / day filters
-// included), one workgroup each by ticket, before k_tail; what is not simple is left to
-// k_tail's exact path. Its own kernel so that big_simple's registers never meet
-// full_windows' and big_exact's: together they spilled k_tail at 1024 threads (52 VGPRs, 244 B
-// of scratch per lane: 1.9 GB of scratch writes per C5 put, profiles/r03e_hbm_c2_c5.json).
-// bstat[bi] = 1 linked (or outside the window), 2 for k_tail's exact path.
-__global__ void __launch_bounds__(TAIL_WG, 1) k_big(Args A) {
+// included), before k_tail; what is not simple is left to k_tail's exact path. Its own kernel so
+// that big_simple's registers never meet full_windows' and big_exact's: together they spilled
+// k_tail at 1024 threads (52 VGPRs, 244 B of scratch per lane: 1.9 GB of scratch writes per C5
+// put, profiles/r03e_hbm_c2_c5.json). Two launches by trace size: k_big<256> takes the traces of
+// at most KB_SMALL spans, four 256-thread workgroups per CU in 37.5 KB of LDS each (a trace's
+// phases are barrier-latency-bound, so four traces in flight beat one 1024-thread workgroup),
+// k_big<1024> the longer ones in 150 KB. The back list is taken 16 entries per ticket; each
+// launch links the entries of its size class. bstat[bi] = 1 linked (or outside the window),
+// 2 for k_tail's exact path.
+constexpr int KB_SMALL_LDS = 38400;
+constexpr int KB_SMALL = (KB_SMALL_LDS - 240) / 81;  // bs_bytes(n) <= KB_SMALL_LDS
+constexpr int KB_BATCH = 16;
+template <int NT>
+__global__ void __launch_bounds__(NT, NT == 256 ? 4 : 1) k_big(Args A) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   __shared__ uint32_t sh_j;
+  constexpr bool SMALL = NT == 256;
   const uint32_t nlarge = A.grest ? *A.grest_n : *A.large_count;
   if (nlarge == 0) return;
-  const size_t lds_bytes = tail_block_bytes(A.days ? 2 : A.window);
-  if (threadIdx.x == 0) sh_j = atomicAdd(A.tick_big, 1u);
+  const size_t lds_bytes = SMALL ? (size_t)KB_SMALL_LDS : tail_block_bytes(A.days ? 2 : A.window);
+  uint32_t* const tick = SMALL ? A.tick_big + 1 : A.tick_big;
   while (true) {
     __syncthreads();
-    const uint32_t j = sh_j;
+    if (threadIdx.x == 0) sh_j = atomicAdd(tick, (uint32_t)KB_BATCH);
     __syncthreads();
-    if (j >= nlarge) break;
-    if (threadIdx.x == 0) sh_j = atomicAdd(A.tick_big, 1u);
-    const uint32_t bi = A.grest ? A.grest[j] : A.big_cap - 1u - j;
-    const uint8_t gs = A.gstat ? A.gstat[bi] : 0;  // the giant tier's verdict (uniform)
-    uint8_t st = gs;
-    if (gs == 0) st = big_one<0, true>(A, lds, lds_bytes, bi, true) ? 1 : 2;
-    if (threadIdx.x == 0) A.bstat[bi] = st;
+    const uint32_t j0 = sh_j;
+    if (j0 >= nlarge) break;
+    for (uint32_t j = j0; j < j0 + KB_BATCH && j < nlarge; ++j) {
+      const uint32_t bi = A.grest ? A.grest[j] : A.big_cap - 1u - j;
+      const uint32_t t = A.big_list[bi];
+      const uint64_t n = A.off[t + 1] - A.off[t];  // (k_link checked the offsets; a flagged trace
+      if (SMALL != (n <= (uint64_t)A.kb_small)) continue;  // has n out of range: the large launch's)
+      const uint8_t gs = A.gstat ? A.gstat[bi] : 0;  // the giant tier's verdict (uniform)
+      uint8_t st = gs;
+      if (gs == 0) st = big_one<0, true, NT>(A, lds, lds_bytes, bi, true) ? 1 : 2;
+      if (threadIdx.x == 0) A.bstat[bi] = st;
+    }
   }
 }
 
@@ -1773,8 +1796,10 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)k_g_join, hipFuncAttributeMaxDynamicSharedMemorySize, GHCAP * 16);
   if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)k_big, hipFuncAttributeMaxDynamicSharedMemorySize,
+    e = hipFuncSetAttribute((const void*)k_big<TAIL_WG>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)std::max(tail_block_bytes(0), std::max(tail_block_bytes(1), tail_block_bytes(2))));
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)k_big<256>, hipFuncAttributeMaxDynamicSharedMemorySize, KB_SMALL_LDS);
   for (int d = 0; d < 2 && e == hipSuccess; ++d)
     for (int w = 0; w < 3 && e == hipSuccess; ++w)
       for (int o = 0; o < 2 && e == hipSuccess; ++o)
@@ -2011,7 +2036,8 @@ __global__ void k_seg_build(const uint64_t* __restrict__ lg_start, const uint32_
                             const uint32_t* __restrict__ big_list, const uint64_t* __restrict__ off,
                             const uint32_t* __restrict__ tseg_big, uint32_t nb, uint32_t nl, uint32_t cap,
                             const uint64_t* __restrict__ cx_win, const uint32_t* __restrict__ tseg_win, uint32_t nw,
-                            uint64_t tbase, uint64_t* __restrict__ src, uint32_t* __restrict__ cnt) {
+                            uint64_t tbase, uint64_t* __restrict__ src, uint32_t* __restrict__ cnt,
+                            uint32_t* __restrict__ status) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t nbl = (uint64_t)nb + nl;
   if (i < W) {
@@ -2020,12 +2046,23 @@ __global__ void k_seg_build(const uint64_t* __restrict__ lg_start, const uint32_
   } else if (i < (uint64_t)W + nbl) {  // big_list's front (wave_big), then its back
     const uint32_t j = (uint32_t)(i - W);
     const uint32_t bi = j < nb ? j : cap - 1u - (j - nb);
-    src[i] = tbase + 2 * off[big_list[bi]];
-    cnt[i] = tseg_big[bi];
+    const uint32_t t = big_list[bi];
+    src[i] = tbase + 2 * off[t];
+    uint32_t c = tseg_big[bi];
+    if ((uint64_t)c > 2 * (off[t + 1] - off[t])) {  // more links than the segment holds: a bug, not data
+      atomicOr(status, ST_INTERNAL);
+      c = 0;
+    }
+    cnt[i] = c;
   } else if (i < (uint64_t)W + nbl + nw) {
     const uint64_t k = i - W - nbl;
     src[i] = tbase + 2 * (cx_win[2 * k] & ((1ull << 48) - 1));
-    cnt[i] = tseg_win[k];
+    uint32_t c = tseg_win[k];
+    if (c > 2 * (uint32_t)(cx_win[2 * k] >> 48)) {
+      atomicOr(status, ST_INTERNAL);
+      c = 0;
+    }
+    cnt[i] = c;
   }
 }
 
@@ -2056,7 +2093,7 @@ static int sparse_finish(zdl_ctx* c, uint32_t ep, uint32_t lW, uint64_t n_spans,
   hipLaunchKernelGGL(k_seg_build, dim3((unsigned)((nseg + 255) / 256)), dim3(256), 0, s, c->lg_start.p, c->lg_n.p, lW,
                      c->big_list.p, off, c->tseg_big.p, nb, nl, (uint32_t)n_traces, c->cx_win.p, c->tseg_win.p, nw,
                      (uint64_t)2 * n_spans,
-                     c->seg_src.p, c->seg_n.p);
+                     c->seg_src.p, c->seg_n.p, c->status.p);
   HIP_TRY(c, hipGetLastError());
   size_t need = 0;
   HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(nullptr, need, c->seg_n.p, c->seg_off.p, (int)nseg, s));
@@ -2176,6 +2213,20 @@ static int giant_run(zdl_ctx* c, Args& A, uint64_t n_spans, uint64_t n_traces) {
 // A lazy put's k_mid / k_tail, when its k_link left them work (flag seq | FLAG_TAIL) or has not
 // finished yet (then they run after it in stream order and find what there is; k_tail compacts
 // and releases seq again). wait: spin for k_link first (zdl_link); otherwise never waits.
+// k_big's two launches (small traces, four workgroups per CU; then the longer ones)
+static int launch_big(zdl_ctx* c, void** kargs, int wmode) {
+  hipError_t be = hipLaunchKernel((const void*)k_big<256>, dim3((unsigned)c->cus * 4), dim3(256), kargs,
+                                  (size_t)KB_SMALL_LDS, c->stream);
+  if (be == hipSuccess)
+    be = hipLaunchKernel((const void*)k_big<TAIL_WG>, dim3(c->grid), dim3(TAIL_WG), kargs, tail_block_bytes(wmode),
+                         c->stream);
+  if (be != hipSuccess) {
+    c->poisoned = true;
+    return hip_fail(c, be, "k_big launch");
+  }
+  return ZDL_OK;
+}
+
 static int resolve_lazy(zdl_ctx* c, bool wait) {
   if (!c->lazy_pending) return ZDL_OK;
   c->lazy_pending = false;
@@ -2202,12 +2253,8 @@ static int resolve_lazy(zdl_ctx* c, bool wait) {
     }
   }
   if (A.bstat) {
-    const hipError_t be = hipLaunchKernel((const void*)k_big, dim3(c->grid), dim3(TAIL_WG), kargs,
-                                          tail_block_bytes(c->lazy_wmode), c->stream);
-    if (be != hipSuccess) {
-      c->poisoned = true;
-      return hip_fail(c, be, "k_big launch");
-    }
+    const int brc = launch_big(c, kargs, c->lazy_wmode);
+    if (brc != ZDL_OK) return brc;
   }
   const hipError_t le = hipLaunchKernel(k_tail_fn(c->lazy_dense, c->lazy_wmode, 0), dim3(c->grid), dim3(TAIL_WG), kargs,
                                         tail_block_bytes(c->lazy_wmode), c->stream);
@@ -2279,6 +2326,13 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   A.tick_mid = ctr + CTR_TICK_MID;
   A.retry_count = ctr + CTR_RETRY;
   A.tick_big = ctr + CTR_TICK_BIG;
+  {
+    static const uint32_t kbs = [] {
+      const char* e = getenv("ZDL_KB_SMALL");  // A/B and tests: 0 = every trace in k_big<1024>
+      return e ? (uint32_t)std::min<long>(std::max<long>(atol(e), 0), KB_SMALL) : (uint32_t)KB_SMALL;
+    }();
+    A.kb_small = kbs;
+  }
   A.ctr_next = c->counters.p + (ep ^ 1u) * CTR_N;
   A.big_cap = (uint32_t)n_traces;
   A.status = c->status.p;
@@ -2459,12 +2513,8 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   }
   ev_record(c, 8);
   if (A.bstat) {
-    const hipError_t be = hipLaunchKernel((const void*)k_big, dim3(grid), dim3(TAIL_WG), kargs, tail_block_bytes(wmode),
-                                          c->stream);
-    if (be != hipSuccess) {
-      c->poisoned = true;
-      return hip_fail(c, be, "k_big launch");
-    }
+    const int brc = launch_big(c, kargs, wmode);
+    if (brc != ZDL_OK) return brc;
   }
   const hipError_t le = hipLaunchKernel(k_tail_fn(c->sparse ? 2 : dense, wmode, c->ord ? 1 : 0), dim3(grid),
                                         dim3(TAIL_WG), kargs, tail_block_bytes(wmode), c->stream);
