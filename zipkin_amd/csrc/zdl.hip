@@ -3245,6 +3245,9 @@ struct PcieSegs {
 };
 __global__ void __launch_bounds__(256) k_pcie_copy(unsigned char* __restrict__ dst, const unsigned char* __restrict__ src,
                                                    PcieSegs g) {
+  // top issue priority: its waves only issue stores and share CUs with the next put's kernels,
+  // which would otherwise starve them (the copy then stretched 2.6 -> 5.6 ms beside a C5 put)
+  __builtin_amdgcn_s_setprio(3);
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x, T = (size_t)gridDim.x * blockDim.x;
   for (int k = 0; k < 4; ++k) {
     const size_t n8 = g.len[k] / 8;
