@@ -41,6 +41,14 @@ class Dictionary:
             self._ranks = None
         return i
 
+    def lowered(self) -> list:
+        """The strings lower-cased (DependencyLink.Builder's parent / child), cached."""
+        lw = getattr(self, "_lowered", None)
+        if lw is None or len(lw) != len(self.strings):
+            lw = [x.lower() for x in self.strings]
+            self._lowered = lw
+        return lw
+
     def ranks(self) -> np.ndarray:
         if self._ranks is None or len(self._ranks) != len(self.strings):
             order = sorted(range(len(self.strings)), key=lambda i: java_string_key(self.strings[i]))

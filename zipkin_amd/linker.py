@@ -202,8 +202,9 @@ class DependencyLinker:
         if self._ctx is None:
             return []
         p, c, n, e = self._ctx.link(self._order())
-        s = self.svc.strings
-        return [DependencyLink.create(s[a], s[b], int(x), int(y)) for a, b, x, y in zip(p, c, n, e)]
+        low = self.svc.lowered()  # DependencyLink.Builder lower-cases (DependencyLink.java:72-82)
+        return [DependencyLink(low[a], low[b], x, y) for a, b, x, y in zip(p.tolist(), c.tolist(), n.tolist(),
+                                                                          e.tolist())]
 
     @staticmethod
     def merge(links: Iterable[DependencyLink], device: int = 0) -> List[DependencyLink]:

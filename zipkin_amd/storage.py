@@ -80,6 +80,9 @@ class InMemoryStorage:
         self.device = device
         self.compact_min = compact_min
         self._linker = DependencyLinker(device)  # owns the dictionaries
+        # the queries' linkers (no window / a time window), kept between queries: a context is
+        # created once and reset per query (creating one per query cost more than the link)
+        self._qlinker = {}
         self._store: Optional[N.Store] = None
         self._decoder = None  # proto3.Proto3Decoder, created on the first accept_proto3
         self._json_decoder = None  # jsonv2.JsonV2Decoder, created on the first accept_json_v2
@@ -167,16 +170,20 @@ class InMemoryStorage:
         _, n_traces = self._store.select(mode)
         if n_traces == 0:
             return []
-        linker = DependencyLinker(self.device, insertion_order=self.insertion_order)
-        linker.svc, linker.ip4, linker.ip6 = self._linker.svc, self._linker.ip4, self._linker.ip6
-        try:
-            ctx = linker._context(window is not None)
-            if window is not None:
-                ctx.set_window(*window)
-            ctx.put_selection(self._store)
-            return linker.link()
-        finally:
-            linker.close()
+        key = window is not None
+        linker = self._qlinker.get(key)
+        if linker is None:
+            linker = DependencyLinker(self.device, insertion_order=self.insertion_order)
+            linker.svc, linker.ip4, linker.ip6 = self._linker.svc, self._linker.ip4, self._linker.ip6
+            self._qlinker[key] = linker
+        fresh = linker._ctx is None
+        ctx = linker._context(key)
+        if not fresh:
+            ctx.reset()  # (a context grown by _context carried counts over: reset drops them too)
+        if window is not None:
+            ctx.set_window(*window)
+        ctx.put_selection(self._store)
+        return linker.link()
 
     def get_dependencies(self, end_ts: Optional[int] = None, lookback: Optional[int] = None):
         """SpanStore.getDependencies(endTs, lookback) (SpanStore.java:85; IMS:323-332), in
@@ -212,6 +219,9 @@ class InMemoryStorage:
 
     def close(self):
         self._linker.close()
+        for q in self._qlinker.values():
+            q.close()
+        self._qlinker = {}
         for d in (self._decoder, self._json_decoder):
             if d is not None:
                 d.close()
