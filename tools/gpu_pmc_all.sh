@@ -18,7 +18,7 @@ run() {  # name timeout command...
   python3 tools/kernel_hbm.py $(ls $O/hs_${n}_$TAG/*kernel_stats.csv $O/hs_${n}_$TAG/*/*kernel_stats.csv 2>/dev/null | head -1) \
     $O/hf_${n}_$TAG $O/hw_${n}_$TAG --json $O/hbm_${n}_$TAG.json --label "$n" > $O/hbm_${n}_$TAG.txt
 }
-B="bench.py --steps 3 --warmup 1 --inflight 1 --no-parity --no-cpu-baseline --no-traffic"
+B="bench.py --steps 3 --warmup 1 --inflight 1 --no-parity --no-cpu-baseline --no-traffic --no-c5"
 run c3 300 python3 $B --config c3 || exit $?
 run c5 400 python3 tools/c5_run.py --no-parity --steps 2 || exit $?
 run json 240 python3 tools/json_decode_run.py --reps 2 || exit $?

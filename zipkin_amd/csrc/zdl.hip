@@ -3293,7 +3293,10 @@ static int rec_download(zdl_ctx* c, uint64_t m) {
     g.off[k] = off[k];
     g.len[k] = len[k];
   }
-  hipLaunchKernelGGL(k_pcie_copy, dim3((unsigned)wgs), dim3(256), 0, c->stream, c->d_rec, c->rec_dev.p, g);
+  // a small list (C3's 250 k links, 6 MB) crosses faster from many workgroups; a large one (C5's
+  // 4.5 M, 107 MB) is left to few, beside the next put
+  const unsigned grid = m * 24 <= ((size_t)16 << 20) ? 128u : (unsigned)wgs;
+  hipLaunchKernelGGL(k_pcie_copy, dim3(grid), dim3(256), 0, c->stream, c->d_rec, c->rec_dev.p, g);
   HIP_TRY(c, hipGetLastError());
   return ZDL_OK;
 }
