@@ -3261,6 +3261,14 @@ __global__ void __launch_bounds__(256) k_pcie_copy(unsigned char* __restrict__ d
 
 // The mapped pinned output columns (parent, child i32; call, err i64) for m links, and their
 // HBM staging copy.
+static bool rec_dma() {
+  static const bool on = [] {
+    const char* e = getenv("ZDL_REC_DMA");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 static int ensure_rec(zdl_ctx* c, uint64_t m) {
   if (m <= c->h_rec_cap) return ZDL_OK;
   c->rec_dev.release();
@@ -3269,8 +3277,12 @@ static int ensure_rec(zdl_ctx* c, uint64_t m) {
   c->d_rec = nullptr;
   c->h_rec_cap = 0;
   const size_t cap = std::max<size_t>((size_t)(m + m / 2 + 1) & ~(size_t)1, 1024);
-  HIP_TRY(c, hipHostMalloc((void**)&c->h_rec, cap * 24, hipHostMallocMapped | hipHostMallocCoherent));
-  HIP_TRY(c, hipHostGetDevicePointer((void**)&c->d_rec, c->h_rec, 0));
+  if (rec_dma()) {  // coarse-grained pinned memory: the copy engine can take it
+    HIP_TRY(c, hipHostMalloc((void**)&c->h_rec, cap * 24, hipHostMallocNonCoherent));
+  } else {
+    HIP_TRY(c, hipHostMalloc((void**)&c->h_rec, cap * 24, hipHostMallocMapped | hipHostMallocCoherent));
+    HIP_TRY(c, hipHostGetDevicePointer((void**)&c->d_rec, c->h_rec, 0));
+  }
   HIP_TRY(c, c->rec_dev.ensure(cap * 24));
   c->h_rec_cap = cap;
   return ZDL_OK;
@@ -3283,6 +3295,13 @@ static int ensure_rec(zdl_ctx* c, uint64_t m) {
 static int rec_download(zdl_ctx* c, uint64_t m) {
   const size_t cap = c->h_rec_cap;
   if (m == 0) return ZDL_OK;
+  if (rec_dma()) {  // ZDL_REC_DMA=1 (A/B): hipMemcpyAsync into coarse-grained pinned memory
+    for (size_t off : {(size_t)0, 4 * cap})
+      HIP_TRY(c, hipMemcpyAsync(c->h_rec + off, c->rec_dev.p + off, m * 4, hipMemcpyDeviceToHost, c->stream));
+    for (size_t off : {8 * cap, 16 * cap})
+      HIP_TRY(c, hipMemcpyAsync(c->h_rec + off, c->rec_dev.p + off, m * 8, hipMemcpyDeviceToHost, c->stream));
+    return ZDL_OK;
+  }
   static const int wgs = [] {
     const char* e = getenv("ZDL_PCIE_WGS");
     return e ? std::max(1, atoi(e)) : 8;  // 8 / 32 / 64: C5 two in flight 6.73 / 7.08 / 7.17 ms
