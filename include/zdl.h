@@ -436,6 +436,10 @@ int          zdl_decode_retry(zdl_decoder* dec, zdl_decoded* out);
  * ip string with an escape, nesting deeper than 64 inside a span; batches up to 4 GiB. */
 int          zdl_decode_json_v2(zdl_decoder* dec, const uint8_t* bytes, uint64_t len, zdl_decoded* out);
 float        zdl_decoder_struct_ms(const zdl_decoder* dec);  /* HIP-event time of the last JSON structure passes */
+/* Spans of the last JSON decode read by the exact reader (the rest took the fast path: compact,
+ * unescaped, no annotations; see zdl_json.inc). Every span when ZDL_JS_EXACT=1 was set at
+ * zdl_decoder_create. Diagnostic. */
+uint64_t     zdl_decoder_exact_spans(const zdl_decoder* dec);
 /* copies the last decode's device columns into the non-NULL host columns of dst */
 int          zdl_decoder_download(zdl_decoder* dec, const zdl_span_cols* dst);
 

@@ -602,3 +602,167 @@ def test_gpu_decode_then_link_large():
     assert got == exp and len(got) > 0
     assert dec.kernel_ms() > 0 and dec.struct_ms() > 0
     dec.close()
+
+
+# ---------------- the fast path against the exact reader (GPU) ----------------
+
+def _dec_exact(d):
+    """A decoder that reads every span with the exact reader (ZDL_JS_EXACT=1 at creation)."""
+    import os
+    os.environ["ZDL_JS_EXACT"] = "1"
+    try:
+        return _dec(d)
+    finally:
+        del os.environ["ZDL_JS_EXACT"]
+
+
+def _compact_edge_span(r) -> str:
+    """A compact span object (the fast path's shape) with edge values: valid ones the fast path
+    reads itself or must hand over (17+ digit numbers, escapes, null, annotations, upper-case
+    keywords), and, rarely, invalid ones (all-zero ids, bad kinds, ports above 65535...)."""
+    bad = r.random() < 0.03
+
+    def pick(good, worse):
+        return r.choice(worse) if bad and r.random() < 0.3 else r.choice(good)
+    tid = pick(["%016x" % r.randrange(1, 1 << 64), "%032x" % r.randrange(1, 1 << 128), "%x" % r.randrange(1, 1 << 70),
+                "00000000000000000000000000000001", "%020x" % r.randrange(1, 1 << 64), "%x" % r.randrange(1, 99)],
+               ["0" * 16, "0" * 32, "", "ABCDEF0123456789", "%033x" % 5])
+    m = [('"traceId"', '"%s"' % tid),
+         ('"id"', '"%s"' % pick(["%016x" % r.randrange(1, 1 << 64), "1", "%x" % r.randrange(1, 1 << 40)],
+                                ["0" * 16, "%017x" % 3, ""]))]
+    if r.random() < 0.7:
+        m.append(('"parentId"', pick(['"%016x"' % r.randrange(1 << 64), '"0000000000000000"', '"a"', "null"], ['""'])))
+    if r.random() < 0.7:
+        m.append(('"kind"', pick(['"CLIENT"', '"SERVER"', '"PRODUCER"', '"CONSUMER"', '"\u0043LIENT"'],
+                                 ['"client"', '"CLIENTX"', '""', '"CONSUME"'])))
+    if r.random() < 0.5:
+        m.append(('"name"', pick(['"get"', '""', '"a\\"b"', '"x y"', "12"], ["true"])))
+    for k in ('"timestamp"', '"duration"'):
+        if r.random() < 0.8:
+            m.append((k, pick([str(r.randrange(1, 1 << 53)), "0", "1704067200000010", "12345678901234567", "-5", "1e3",
+                               str(r.randrange(10 ** 15, 10 ** 16)), '"77"', "9223372036854775807"],
+                              ["0123", "1.5", "99999999999999999999", '"x"'])))
+
+    def ep():
+        f = []
+        if r.random() < 0.8:
+            f.append('"serviceName":%s' % pick(['"svc-%d"' % r.randrange(9), '""', '"Svc"', '"s\\u0041"', "null"], ["[]"]))
+        if r.random() < 0.6:
+            f.append('"ipv4":%s' % r.choice(['"10.0.0.%d"' % r.randrange(256), '"1.2.3"', '""', '"::ffff:1.2.3.4"',
+                                             '"01.2.3.4"', '"256.1.1.1"', '"::1.2.3.4"']))
+        if r.random() < 0.3:
+            f.append('"ipv6":%s' % r.choice(['"2001:db8::1"', '"::1"', '"fe80::1:2:3:4:5:6:7"', '"1.2.3.4"', '"zz"',
+                                             '"1:2:3:4:5:6:7:8"', '"::"']))
+        if r.random() < 0.5:
+            f.append('"port":%s' % pick(["0", "80", "65535", "-1", "8080", "00"[:1]], ["65536", "1.5"]))
+        r.shuffle(f)
+        return "{" + ",".join(f) + "}"
+    if r.random() < 0.9:
+        m.append(('"localEndpoint"', ep()))
+    if r.random() < 0.6:
+        m.append(('"remoteEndpoint"', ep()))
+    if r.random() < 0.3:
+        m.append(('"tags"', pick(['{"error":""}', '{}', '{"http.path":"/x","error":"boom"}', '{"a":1}', '{"err":"x"}',
+                                  '{"\\u0065rror":"x"}'], ['{"error":null}'])))
+    if r.random() < 0.1:
+        m.append(('"annotations"', '[{"timestamp":1,"value":"ws"}]'))
+    for k in ('"shared"', '"debug"'):
+        if r.random() < 0.2:
+            m.append((k, pick(["true", "false", "TRUE", "null"], ["1"])))
+    if r.random() < 0.05:
+        m.append(('"unknown"', '"x"'))
+    r.shuffle(m)
+    return "{" + ",".join(k + ":" + v for k, v in m) + "}"
+
+
+def _mixed_list(r, n) -> bytes:
+    sp = rand_batch(r, n)
+    objs = []
+    for s in sp:
+        x = r.random()
+        if x < 0.5:
+            objs.append(J.write_list([s])[1:-1].decode())
+        elif x < 0.8:
+            objs.append(_compact_edge_span(r))
+        else:
+            objs.append(noisy_span(r, s))
+    return ("[" + ",".join(objs) + "]").encode()
+
+
+def _d2h(ptr, n, dtype):
+    import ctypes as C
+    hip = C.CDLL("libamdhip64.so")
+    out = np.empty(n, dtype)
+    if n:
+        assert hip.hipMemcpy(C.c_void_p(out.ctypes.data), C.c_void_p(ptr), C.c_size_t(out.nbytes), 2) == 0
+    return out
+
+
+def _decode_outcome(dec, data):
+    """("ok", every column incl. the trace ids' high halves and widths) or (error kind, message)."""
+    from zipkin_amd import _native as N
+    try:
+        b = dec.decode(data)
+    except N.ReferenceIllegalArgumentException as e:
+        return "iae", str(e)
+    except N.ZdlError as e:
+        return "err%d" % e.code, str(e)
+    n = int(b.n_spans)
+    cols = dec._dec.download(n) if n else {}
+    if n:
+        cols["trace_hi"] = _d2h(b.dev_trace_hi, n, np.uint64)
+        cols["trace_wide"] = _d2h(b.dev_trace_wide, n, np.uint8)
+    return "ok", cols
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(6))
+def test_gpu_fast_path_matches_exact_reader(seed):
+    """Compact spans (the fast path), edge values and noisy spans mixed in one list: the default
+    decoder (fast path + exact hand-over) and an all-exact decoder give the same columns, the same
+    dictionaries and the same first error."""
+    r = random.Random(1000 + seed)
+    fast_seen = 0
+    for k in range(40):
+        data = _mixed_list(r, r.randrange(1, 300))
+        if k % 4 == 3:
+            data = mutate(r, data)
+        da, db = fresh(), fresh()
+        fa, ex = _dec(da), _dec_exact(db)
+        a, b = _decode_outcome(fa, data), _decode_outcome(ex, data)
+        assert a[0] == b[0], (a[0], b[0], a[1] if a[0] != "ok" else "", b[1] if b[0] != "ok" else "")
+        if a[0] == "ok":
+            assert sorted(a[1]) == sorted(b[1])
+            for c in a[1]:
+                np.testing.assert_array_equal(a[1][c], b[1][c], err_msg=c)
+            assert [x.strings for x in da] == [x.strings for x in db]
+            fast_seen += len(a[1].get("id", ())) - fa.exact_spans()
+        else:
+            assert a[1] == b[1]
+        fa.close()
+        ex.close()
+    assert fast_seen > 0
+
+
+@pytest.mark.gpu
+def test_gpu_fast_path_takes_compact_lists():
+    """The writer's compact encoding without annotations stays on the fast path entirely; with
+    annotations those spans (only) go to the exact reader."""
+    from zipkin_amd import synth
+    w = synth.C2.scaled(300)
+    cols = synth.generate(w)
+    data = synth.encode_json_v2(cols, synth.service_names(w)).tobytes()
+    d, o = fresh(), fresh()
+    dec = _dec(d)
+    b = dec.decode(data)
+    assert b.n_spans == cols.n_spans and dec.exact_spans() == 0
+    dec.close()
+    dec = _dec(d := fresh())
+    r = random.Random(3)
+    sp = [s for s in rand_batch(r, 400)]
+    data = J.write_list(sp)
+    assert_same(dec.decode_columns(data), oracle_columns(data, *o))
+    n_ann = sum(1 for s in sp if s.annotations)
+    n_esc = sum(1 for s in sp if b"\\" in J.write_list([s]))
+    assert dec.exact_spans() <= n_ann + n_esc + 1, (dec.exact_spans(), n_ann, n_esc)
+    dec.close()

@@ -37,7 +37,7 @@ def main():
                   f"call {dt:.1f} ms", flush=True)
         else:
             print(f"rep {i}: {b.n_spans} spans, {len(data) / 1e9:.2f} GB, structure {dec.struct_ms():.2f} ms, "
-                  f"spans {dec.kernel_ms():.2f} ms, call {dt:.1f} ms", flush=True)
+                  f"spans {dec.kernel_ms():.2f} ms ({dec.exact_spans()} exact), call {dt:.1f} ms", flush=True)
     dec.close()
 
 

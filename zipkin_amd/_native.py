@@ -48,7 +48,7 @@ EXPORTS = (
     "zdl_decoder_dict_size", "zdl_decoder_missing", "zdl_decode_proto3", "zdl_decode_proto3_retry",
     "zdl_decoder_download", "zdl_decoder_kernel_ms", "zdl_put_mysql_rows", "zdl_rows_last_error",
     "zdl_comm_unique_id", "zdl_comm_init", "zdl_put_spans_device_multi", "zdl_device_count", "zdl_shard_of",
-    "zdl_tree_export", "zdl_tree_reasons", "zdl_decode_json_v2", "zdl_decode_retry", "zdl_decoder_struct_ms",
+    "zdl_tree_export", "zdl_tree_reasons", "zdl_decode_json_v2", "zdl_decode_retry", "zdl_decoder_struct_ms", "zdl_decoder_exact_spans",
     "zdl_link_start", "zdl_link_finish",
 )
 ZDL_ABI_VERSION = 4
@@ -201,6 +201,8 @@ def lib() -> C.CDLL:
     L.zdl_decode_retry.argtypes = [vp, C.POINTER(Decoded)]
     L.zdl_decoder_struct_ms.restype = C.c_float
     L.zdl_decoder_struct_ms.argtypes = [vp]
+    L.zdl_decoder_exact_spans.restype = C.c_uint64
+    L.zdl_decoder_exact_spans.argtypes = [vp]
     L.zdl_decoder_download.argtypes = [vp, C.POINTER(SpanCols)]
     L.zdl_put_mysql_rows.argtypes = [vp, C.POINTER(MysqlRows), u64, vp, u32]
     L.zdl_put_mysql_rows.restype = C.c_int
@@ -602,6 +604,10 @@ class Decoder:
 
     def struct_ms(self) -> float:
         return float(self._L.zdl_decoder_struct_ms(self.h))
+
+    def exact_spans(self) -> int:
+        """Spans of the last JSON decode the exact reader took (the rest: the fast path)."""
+        return int(self._L.zdl_decoder_exact_spans(self.h))
 
     def close(self):
         if getattr(self, "h", None):

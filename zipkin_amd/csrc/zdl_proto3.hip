@@ -568,6 +568,9 @@ struct zdl_decoder {
   DBuf<uint32_t> js_cnt;
   DBuf<uint64_t> js_off, js_starts;
   DBuf<uint8_t> js_tmp;  // hipCUB scan scratch
+  DBuf<uint32_t> js_list;  // spans k_js_fast hands to the exact reader (their count: status[2])
+  uint64_t js_n_exact = 0;  // that count for the last JSON decode
+  bool js_exact = false;             // ZDL_JS_EXACT=1: every span through the exact reader (A/B, tests)
   HBuf<unsigned long long> js_h;
   uint64_t js_open = 0;  // the opening '['
   float struct_ms = 0.f;  // HIP-event time of the structural passes of the last JSON decode
@@ -626,23 +629,33 @@ int run_kernel(zdl_decoder* d, zdl_decoded* out) {
   const uint64_t n = d->n;
   if (n) {
     DEC_TRY(d, hipMemsetAsync(d->status.p, 0xFF, 8, s));
-    DEC_TRY(d, hipMemsetAsync(d->status.p + 1, 0, 8, s));
+    DEC_TRY(d, hipMemsetAsync(d->status.p + 1, 0, 16, s));
     Dict dict{d->slots.p, d->arena.p, d->cap ? d->cap - 1 : 0};
     Out o{d->lo.p,   d->id.p, d->pid.p, d->lsvc.p,     d->rsvc.p,     d->ip4.p,    d->ip6.p,
           d->pf.p,   d->ts.p, d->miss.p, d->miss_off.p, d->miss_len.p, d->status.p, (uint32_t*)(d->status.p + 1),
           d->hi.p, d->fmt == 1 ? d->wide.p : nullptr};
     DEC_TRY(d, hipEventRecord(d->ev[0], s));
-    if (d->fmt == 1)
-      zjs::k_js_spans<<<(unsigned)((n + zjs::kSpanWG - 1) / zjs::kSpanWG), zjs::kSpanWG, 0, s>>>(
-          d->buf.p, d->len, d->js_starts.p, (uint32_t)n, d->js_open, d->js_misc.p, dict, o);
-    else
+    const unsigned nb = (unsigned)((n + zjs::kSpanWG - 1) / zjs::kSpanWG);
+    if (d->fmt == 1 && d->js_exact) {
+      zjs::k_js_spans<<<nb, zjs::kSpanWG, 0, s>>>(d->buf.p, d->len, d->js_starts.p, (uint32_t)n, d->js_open,
+                                                  d->js_misc.p, dict, o);
+    } else if (d->fmt == 1) {  // the common shape fast, the rest exact
+      DEC_TRY(d, d->js_list.ensure(n));
+      zjs::k_js_fast<<<nb, zjs::kSpanWG, 0, s>>>(d->buf.p, d->len, d->js_starts.p, (uint32_t)n, d->js_open,
+                                                 d->js_misc.p, dict, o, d->js_list.p, (uint32_t*)(d->status.p + 2));
+      DEC_TRY(d, hipGetLastError());
+      zjs::k_js_spans_list<<<nb < 1024u ? nb : 1024u, zjs::kSpanWG, 0, s>>>(
+          d->buf.p, d->len, d->js_starts.p, (uint32_t)n, d->js_open, d->js_misc.p, dict, o, d->js_list.p,
+          (const uint32_t*)(d->status.p + 2));
+    } else
       k_proto3_spans<<<(unsigned)((n + kBlock - 1) / kBlock), kBlock, 0, s>>>(d->buf.p, d->len, d->start.p, d->slen.p,
                                                                               (uint32_t)n, dict, o);
     DEC_TRY(d, hipGetLastError());
     DEC_TRY(d, hipEventRecord(d->ev[1], s));
-    DEC_TRY(d, hipMemcpyAsync(d->status_h.p, d->status.p, 16, hipMemcpyDeviceToHost, s));
+    DEC_TRY(d, hipMemcpyAsync(d->status_h.p, d->status.p, 24, hipMemcpyDeviceToHost, s));
     DEC_TRY(d, hipStreamSynchronize(s));
     DEC_TRY(d, hipEventElapsedTime(&d->kernel_ms, d->ev[0], d->ev[1]));
+    if (d->fmt == 1) d->js_n_exact = d->js_exact ? n : (uint32_t)d->status_h.p[2];
     const unsigned long long fe = d->status_h.p[0];
     if (fe != kNoErr && d->fmt == 1)  // (span << 2 | after-the-span << 1 | iae): the lowest decides
       return (fe & 1) ? dfail(d, ZDL_EREF_IAE, "reference throws IllegalArgumentException reading List<Span> from json (span " +
@@ -708,8 +721,10 @@ zdl_decoder* zdl_decoder_create(int device) {
   zdl_decoder* d = new (std::nothrow) zdl_decoder();
   if (!d) return nullptr;
   d->device = device;
+  const char* ex = std::getenv("ZDL_JS_EXACT");
+  d->js_exact = ex && ex[0] == '1';
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess ||
-      d->status.ensure(2) != hipSuccess || d->status_h.ensure(2) != hipSuccess ||
+      d->status.ensure(3) != hipSuccess || d->status_h.ensure(3) != hipSuccess ||
       hipEventCreate(&d->ev[0]) != hipSuccess || hipEventCreate(&d->ev[1]) != hipSuccess ||
       hipEventCreate(&d->ev_s[0]) != hipSuccess || hipEventCreate(&d->ev_s[1]) != hipSuccess) {
     if (d->stream) (void)hipStreamDestroy(d->stream);
@@ -751,6 +766,7 @@ uint64_t zdl_decoder_dict_size(const zdl_decoder* d) { return d ? d->keys.size()
 float zdl_decoder_kernel_ms(const zdl_decoder* d) { return d ? d->kernel_ms : 0.f; }
 
 float zdl_decoder_struct_ms(const zdl_decoder* d) { return d ? d->struct_ms : 0.f; }
+uint64_t zdl_decoder_exact_spans(const zdl_decoder* d) { return d ? d->js_n_exact : 0; }
 
 int zdl_decoder_missing(const zdl_decoder* d, uint64_t i, int* kind, const uint8_t** key, uint32_t* len) {
   if (!d || i >= d->missing.size() || !kind || !key || !len) return ZDL_EINVAL;

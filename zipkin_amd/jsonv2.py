@@ -142,5 +142,8 @@ class JsonV2Decoder:
     def struct_ms(self) -> float:
         return self._dec.struct_ms()
 
+    def exact_spans(self) -> int:
+        return self._dec.exact_spans()
+
     def close(self):
         self._dec.close()
