@@ -47,6 +47,9 @@ struct Slot {
   uint64_t h;
   uint32_t koff;  // kNoKey = empty
   int32_t id;
+  uint32_t len, kind;
+  uint64_t k0, k1;  // the key's first 16 bytes (little-endian, zero-padded): keys up to 16 bytes
+                    // compare here, without the arena
 };
 
 struct Dict {
@@ -268,10 +271,30 @@ __device__ __forceinline__ int32_t lookup(const Dict& d, int kind, Get p, uint32
     const uint32_t kl = (uint32_t)k[0] | (uint32_t)k[1] << 8 | (uint32_t)k[2] << 16 | (uint32_t)k[3] << 24;
     if (kl != n || k[4] != (uint8_t)kind) continue;
     bool eq = true;
-    for (uint32_t j = 0; j < n && eq; ++j) eq = k[5 + j] == p(j);
+    if (n <= 24) {  // every byte at once: one memory round trip, not one per byte
+#pragma unroll
+      for (uint32_t j = 0; j < 24; ++j)
+        if (j < n) eq &= k[5 + j] == p(j);
+    } else {
+      for (uint32_t j = 0; j < n && eq; ++j) eq = k[5 + j] == p(j);
+    }
     if (eq) return s.id;
   }
   return -2;
+}
+
+// A key of n <= 16 bytes given as two little-endian words (zero past n): its hash
+__device__ __forceinline__ uint64_t key_hash16(int kind, uint64_t w0, uint64_t w1, uint32_t n) {
+  return key_hash(kind, [&](uint32_t j) { return (uint32_t)((j < 8 ? w0 >> (8 * j) : w1 >> (8 * (j - 8))) & 0xFFu); },
+                  n);
+}
+// ... and its id from the slot at (h & mask) when that slot is the key's (nearly always): the
+// first probe is issued by the caller for several keys at once; -3 = probe on (lookup())
+__device__ __forceinline__ int32_t slot_match(const Slot& s, uint64_t h, int kind, uint64_t w0, uint64_t w1,
+                                              uint32_t n) {
+  if (s.koff == kNoKey) return -2;
+  if (s.h == h && s.len == n && s.kind == (uint32_t)kind && s.k0 == w0 && s.k1 == w1) return s.id;
+  return -3;
 }
 
 __global__ void __launch_bounds__(kBlock) k_proto3_spans(const uint8_t* __restrict__ buf, uint64_t len,
@@ -597,7 +620,7 @@ int upload_dict(zdl_decoder* d) {
   if (!d->dirty) return ZDL_OK;
   uint32_t cap = 16;
   while (cap < 2 * d->keys.size() + 2) cap <<= 1;
-  std::vector<Slot> sl(cap, Slot{0, kNoKey, -1});
+  std::vector<Slot> sl(cap, Slot{0, kNoKey, -1, 0, 0, 0, 0});
   for (const auto& kv : d->keys) {
     const std::string& k = kv.first;  // k[0] = kind, then the key bytes
     const uint32_t koff = (uint32_t)d->arena_h.size();
@@ -608,7 +631,9 @@ int upload_dict(zdl_decoder* d) {
     const uint64_t h = key_hash((uint8_t)k[0], [kb](uint32_t j) { return kb[j]; }, kl);
     uint32_t i = (uint32_t)h & (cap - 1);
     while (sl[i].koff != kNoKey) i = (i + 1) & (cap - 1);
-    sl[i] = Slot{h, koff, kv.second};
+    uint64_t kw[2] = {0, 0};
+    for (uint32_t j = 0; j < kl && j < 16; ++j) kw[j >> 3] |= (uint64_t)kb[j] << (8 * (j & 7));
+    sl[i] = Slot{h, koff, kv.second, kl, (uint32_t)(uint8_t)k[0], kw[0], kw[1]};
   }
   DEC_TRY(d, d->slots.ensure(cap));
   DEC_TRY(d, d->arena.ensure(d->arena_h.size()));
