@@ -58,6 +58,7 @@ struct Dict {
   uint32_t mask;  // capacity - 1
 };
 
+// Key hash (FNV-1a over the kind and the bytes): the host and both decoders use this function
 template <class Get>
 __host__ __device__ __forceinline__ uint64_t key_hash(int kind, Get get, uint32_t n) {
   uint64_t h = 1469598103934665603ull ^ (uint64_t)(kind + 1);
@@ -947,7 +948,7 @@ int zdl_decode_json_v2(zdl_decoder* d, const uint8_t* data, uint64_t len, zdl_de
       k_js_starts_exact<1><<<g4, 256, 0, s>>>(d->buf.p, len, nblk, d->js_fn.p, d->js_lpre.p, d->js_gst.p, nullptr,
                                                d->js_off.p, d->js_starts.p);
     else
-      k_js_gather<<<g4, 256, 0, s>>>(d->js_slots.p, d->js_cnt.p, d->js_off.p, nblk, d->js_starts.p);
+      k_js_gather<<<(nblk + 15) / 16, 256, 0, s>>>(d->js_slots.p, d->js_cnt.p, d->js_off.p, nblk, d->js_starts.p);
     k_js_before<<<(unsigned)((total + 255) / 256), 256, 0, s>>>(d->js_starts.p, total, d->js_misc.p, d->js_misc.p + 1);
     DEC_TRY(d, hipGetLastError());
   }
