@@ -98,8 +98,9 @@ def json_v2_leg(cols, w, device, doff, links, reps=3):
     """Decode the batch's JSON v2 encoding (V2SpanWriter member order, synth.encode_json_v2) on the
     device, then link the decoded columns with the batch's trace offsets: the links must equal the
     columnar path's `links` by service name. Device time = the structure passes (block functions,
-    scans, object starts) + k_js_spans, by HIP events; the call time adds the PCIe upload and the
-    trace-id/timestamp download. Compulsory traffic: the bytes once + 52 B/span of columns."""
+    scans, object starts) + k_js_fast / k_js_spans_list, by HIP events; the call time adds the PCIe upload and the
+    trace-id/timestamp download. Compulsory traffic: the bytes once + 52 B/span of columns.
+    `exact_spans`: spans the exact reader took instead of the fast path (0 for the writer's shape)."""
     from zipkin_amd import synth
     from zipkin_amd.columnar import Dictionary
     from zipkin_amd import _native as N
@@ -117,6 +118,7 @@ def json_v2_leg(cols, w, device, doff, links, reps=3):
         ks.append(dec.kernel_ms())
         ss.append(dec.struct_ms())
     km, sm, cm = float(np.median(ks)), float(np.median(ss)), float(np.median(cs)) * 1e3
+    n_exact = dec.exact_spans()
     svc = dicts[0]
     ctx = N.Context(max(len(svc), 1), device=device)
     dptr = {k: getattr(b.dev, k) for k in ("id", "parent_id", "local_svc", "remote_svc", "local_ip4",
@@ -134,7 +136,8 @@ def json_v2_leg(cols, w, device, doff, links, reps=3):
     return {"bytes": len(data), "spans": b.n_spans, "structure_ms": sm, "spans_kernel_ms": km, "device_ms": dev_ms,
             "call_ms": cm, "spans_per_s": b.n_spans / (dev_ms * 1e-3), "device_gbs": algo / (dev_ms * 1e-3) / 1e9,
             "roofline_frac": algo / (dev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes": algo,
-            "call_spans_per_s": b.n_spans / (cm * 1e-3), "parity": "same links" if got == exp else "MISMATCH"}
+            "call_spans_per_s": b.n_spans / (cm * 1e-3), "exact_spans": n_exact,
+            "parity": "same links" if got == exp else "MISMATCH"}
 
 
 def store_leg(cols, S, device, links, names, reps=5):
