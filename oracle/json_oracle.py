@@ -702,7 +702,8 @@ def _read_span(r: _Reader) -> Span:
                 raise IllegalArgument(str(ex))
             continue
         if key == "id":
-            sid = _id_norm(r.next_string())
+            sid_raw = r.next_string()
+            sid = _id_norm(sid_raw)  # the Builder's checks, once: Span.create gets the text as read
             continue
         if r.peek_null():
             r.skip_value()
@@ -761,7 +762,7 @@ def _read_span(r: _Reader) -> Span:
     r.end_object()
     if trace_id is None or sid is None:  # Span.Builder.build: IllegalStateException
         raise IllegalArgument("Missing :" + (" traceId" if trace_id is None else "") + (" id" if sid is None else ""))
-    return Span.create(trace_id, sid, pid, kind, name=name, timestamp=max(ts, 0), duration=max(dur, 0),
+    return Span.create(trace_id, sid_raw, pid, kind, name=name, timestamp=max(ts, 0), duration=max(dur, 0),
                        local_endpoint=local, remote_endpoint=remote, annotations=tuple(ann),
                        tags=tags, shared=shared, debug=debug)
 

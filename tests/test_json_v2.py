@@ -134,6 +134,15 @@ def test_trace_id_high_read_from_trace_id_field():  # readsTraceIdHighFromTraceI
     assert a == [b[0].to_builder(trace_id="48485a3953bb61246b221d5bc9e6496c")]
 
 
+def test_short_zero_id_is_kept():
+    """Span.Builder.id("0") pads to 16 zeros and keeps it (Span.java:474-483: only a 16-zero text
+    is "all zeros"); the decoder reads it once, as V2SpanReader does."""
+    sp = J.read_list(b'[{"traceId":"a","id":"0"}]')
+    assert sp[0].id == "0" * 16
+    with pytest.raises(J.IllegalArgument):
+        J.read_list(b'[{"traceId":"a","id":"0000000000000000"}]')
+
+
 def test_empty_and_malformed():  # falseOnEmpty_inputSpans / niceErrorOnMalformed_inputSpans
     assert J.read_list(b"") == []
     assert J.read_list(b"[]") == []
@@ -628,7 +637,7 @@ def _compact_edge_span(r) -> str:
                 "00000000000000000000000000000001", "%020x" % r.randrange(1, 1 << 64), "%x" % r.randrange(1, 99)],
                ["0" * 16, "0" * 32, "", "ABCDEF0123456789", "%033x" % 5])
     m = [('"traceId"', '"%s"' % tid),
-         ('"id"', '"%s"' % pick(["%016x" % r.randrange(1, 1 << 64), "1", "%x" % r.randrange(1, 1 << 40)],
+         ('"id"', '"%s"' % pick(["%016x" % r.randrange(1, 1 << 64), "1", "%x" % r.randrange(1, 1 << 40), "0"],
                                 ["0" * 16, "%017x" % 3, ""]))]
     if r.random() < 0.7:
         m.append(('"parentId"', pick(['"%016x"' % r.randrange(1 << 64), '"0000000000000000"', '"a"', "null"], ['""'])))
