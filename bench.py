@@ -261,7 +261,7 @@ def _small_bytes(sizes, n_traces):
     return BYTES_PER_SPAN * int(sizes[sizes <= 64].sum()) + BYTES_PER_TRACE * (n_traces + 1)
 
 
-def c5_leg(device, steps=8, parity=True, threads=16):
+def c5_leg(device, steps=8, parity=True, threads=16, host_threads=1):
     """BASELINE.json configs[4] (C5: 10 000 services, Zipf(1.1), depth 64, fan-out <= 1000,
     Pareto(1.2) trace sizes clipped to [1, 200 000]: 81.1M spans / 16M traces) on one GPU, a
     sparse context (the link list sorted by cell, no S x S table). One step = reset, put of the
@@ -296,14 +296,36 @@ def c5_leg(device, steps=8, parity=True, threads=16):
         put(c)
         c.link_finish(copy=False)
     torch.cuda.synchronize(dev)
+    # one host thread per context (ctypes drops the GIL in every libzdl call): a context's host
+    # waits (the giant tier reads two counts back) do not hold up the other context's launches
+    import threading
+    outs = [None, None]
+    errs = []
+
+    def worker(j):
+        try:
+            for _ in range(j, steps, 2):
+                put(ctxs[j])
+                outs[j] = ctxs[j].link_finish(copy=False)
+        except Exception as e:  # surfaced after the join
+            errs.append(e)
+    th = [threading.Thread(target=worker, args=(j,)) for j in range(2)]
     t1 = time.perf_counter()
-    for k in range(steps):
-        put(ctxs[k % 2])
-        if k:
-            out = ctxs[(k - 1) % 2].link_finish(copy=False)
-    out = ctxs[(steps - 1) % 2].link_finish(copy=False)
+    if host_threads == 2:
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+    else:  # one host thread alternating the contexts (A/B)
+        for k in range(steps):
+            put(ctxs[k % 2])
+            if k:
+                outs[(k - 1) % 2] = ctxs[(k - 1) % 2].link_finish(copy=False)
+        outs[(steps - 1) % 2] = ctxs[(steps - 1) % 2].link_finish(copy=False)
     ms = (time.perf_counter() - t1) / steps * 1e3
-    out = tuple(a.copy() for a in out)
+    if errs:
+        raise errs[0]
+    out = tuple(a.copy() for a in outs[(steps - 1) % 2])
     # the phases of one step run alone (HIP events)
     c = ctxs[0]
     put(c)
@@ -336,14 +358,15 @@ def c5_leg(device, steps=8, parity=True, threads=16):
     for k in ("sparse_merge", "link_compact"):
         kern[k] = {"ms": last[k]}
     res = {"workload": w.name, "spans": cols.n_spans, "traces": cols.n_traces, "services": S,
-           "ms_per_step": ms, "spans_per_s": cols.n_spans / (ms * 1e-3), "inflight": 2,
+           "ms_per_step": ms, "spans_per_s": cols.n_spans / (ms * 1e-3), "inflight": 2, "host_threads": host_threads,
            "ms_per_step_serial": serial_ms,
            "step_roofline_frac": (BYTES_PER_SPAN * cols.n_spans + BYTES_PER_TRACE * (cols.n_traces + 1))
            / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
            "steps": steps, "giant_min": gmin, "links": int(len(out[0])), "phases": kern,
            "note": "phase times: HIP events of one step run alone (the giant tier's include its two host syncs); "
-                   "step: wall clock of reset + put + link into pinned host columns, two steps in flight "
-                   "(zdl_link_start / zdl_link_finish: a step's link list crosses PCIe during the next put)",
+                   "step: wall clock of reset + put + link into pinned host columns, two contexts in flight "
+                   "(host_threads 1: one thread alternating them, zdl_link_start / zdl_link_finish; 2: a thread "
+                   "each), a step's link list crossing PCIe while the other context's put runs",
            "parity": None}
     if parity:
         from oracle import ref
@@ -514,6 +537,8 @@ def main():
     ap.add_argument("--no-json", action="store_true", help="skip the JSON v2 ingest side leg")
     ap.add_argument("--no-store", action="store_true", help="skip the resident-store getDependencies side leg")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 (high-cardinality) side leg")
+    ap.add_argument("--c5-host-threads", type=int, default=1, choices=(1, 2),
+                    help="C5 leg: one host thread per context (2) or one alternating both (1)")
     ap.add_argument("--no-traffic", action="store_true",
                     help="skip the rocprofv3 FETCH_SIZE / WRITE_SIZE passes behind roofline.traffic")
     ap.add_argument("--pmc-probe", action="store_true", help=argparse.SUPPRESS)  # child of pmc_traffic
@@ -718,7 +743,7 @@ def main():
             f"host columns {h2d['e2e_ms']:.2f} ms")
     c5 = None
     if side and not args.no_c5:
-        c5 = c5_leg(local, parity=not args.no_parity, threads=cpu_info()["usable"])
+        c5 = c5_leg(local, parity=not args.no_parity, threads=cpu_info()["usable"], host_threads=args.c5_host_threads)
         log(f"c5: {c5['ms_per_step']:.2f} ms/step ({c5['spans_per_s']:.3e} spans/s), links {c5['parity']}, "
             + ", ".join(f"{k} {v['ms']:.3f} ms" for k, v in c5["phases"].items() if v["ms"] is not None))
     parity = None
