@@ -596,7 +596,7 @@ struct zdl_decoder {
   uint64_t js_n_exact = 0;  // that count for the last JSON decode
   bool js_exact = false;             // ZDL_JS_EXACT=1: every span through the exact reader (A/B, tests)
   int js_global = 2;  // the fast path reads its objects from HBM / the caches at 4 waves per SIMD
-                      // (ZDL_JS_GLOBAL=2, default), at the registers' 3 (1), or from the block's LDS
+                      // (ZDL_JS_GLOBAL=2, default; 3 / 4: 5 / 6 waves), at the registers' 3 (1), or from the block's LDS
                       // window (0: 2 waves per SIMD); A/B in profiles/r03t_js_fast_variants.log
   HBuf<unsigned long long> js_h;
   uint64_t js_open = 0;  // the opening '['
@@ -672,6 +672,12 @@ int run_kernel(zdl_decoder* d, zdl_decoded* out) {
       DEC_TRY(d, d->js_list.ensure(n));
       if (d->js_global == 2)
         zjs::k_js_fast_g<4><<<nb, zjs::kSpanWG, 0, s>>>(d->buf.p, d->len, d->js_starts.p, (uint32_t)n, d->js_open,
+                                                        d->js_misc.p, dict, o, d->js_list.p, (uint32_t*)(d->status.p + 2));
+      else if (d->js_global == 3)
+        zjs::k_js_fast_g<5><<<nb, zjs::kSpanWG, 0, s>>>(d->buf.p, d->len, d->js_starts.p, (uint32_t)n, d->js_open,
+                                                        d->js_misc.p, dict, o, d->js_list.p, (uint32_t*)(d->status.p + 2));
+      else if (d->js_global == 4)
+        zjs::k_js_fast_g<6><<<nb, zjs::kSpanWG, 0, s>>>(d->buf.p, d->len, d->js_starts.p, (uint32_t)n, d->js_open,
                                                         d->js_misc.p, dict, o, d->js_list.p, (uint32_t*)(d->status.p + 2));
       else if (d->js_global)
         zjs::k_js_fast_g<1><<<nb, zjs::kSpanWG, 0, s>>>(d->buf.p, d->len, d->js_starts.p, (uint32_t)n, d->js_open,
@@ -760,7 +766,7 @@ zdl_decoder* zdl_decoder_create(int device) {
   const char* ex = std::getenv("ZDL_JS_EXACT");
   d->js_exact = ex && ex[0] == '1';
   const char* jg = std::getenv("ZDL_JS_GLOBAL");
-  if (jg && jg[0] >= '0' && jg[0] <= '2') d->js_global = jg[0] - '0';
+  if (jg && jg[0] >= '0' && jg[0] <= '4') d->js_global = jg[0] - '0';
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess ||
       d->status.ensure(3) != hipSuccess || d->status_h.ensure(3) != hipSuccess ||
       hipEventCreate(&d->ev[0]) != hipSuccess || hipEventCreate(&d->ev[1]) != hipSuccess ||
