@@ -245,6 +245,34 @@ def mysql_rows_leg(cols, S, device, max_spans=2_000_000, reps=3):
             "spans_per_s": m / t, "note": "rows host-resident (PCIe-inclusive), timing only"}
 
 
+def put_trace_leg(cols, S, device, links, reps=3):
+    """DependencyLinker.putTrace called once per trace, as the reference's callers loop
+    (InMemoryStorage.java:340, AggregateDependencies.java:81): libzdl_synth's native driver
+    calls zdl_put_trace for each of the batch's traces in order (what a JNI shim does after
+    packing a trace), then zdl_link. The traces are staged into pinned CSR batches and put one
+    launch per batch. PCIe-inclusive (host columns in), timed wall clock; the
+    links must equal the columnar path's. Compare with cpu_baseline.single_thread (one
+    DependencyLinker restated in C++ over the same batch)."""
+    from zipkin_amd import _native as N
+    from zipkin_amd import synth
+    ctx = N.Context(S, device=device)
+    ts = []
+    out = None
+    for k in range(reps + 1):
+        ctx.reset()
+        t0 = time.perf_counter()
+        synth.put_trace_loop(ctx, cols)
+        out = ctx.link()
+        ts.append(time.perf_counter() - t0)
+    ctx.close()
+    t = float(np.median(ts[1:]))
+    return {"traces": cols.n_traces, "spans": cols.n_spans, "calls": cols.n_traces, "ms": t * 1e3,
+            "spans_per_s": cols.n_spans / t, "us_per_call": t / cols.n_traces * 1e6,
+            "parity": "same links" if _same_links(out, links) else "MISMATCH",
+            "note": "one zdl_put_trace per trace from native code (the JNI caller's loop) + zdl_link; host "
+                    "columns, PCIe-inclusive; staged in pinned batches of 2^20 spans"}
+
+
 def _sorted_links(p, c, n, e):
     o = np.lexsort((c, p))
     return p[o], c[o], n[o], e[o]
@@ -282,14 +310,18 @@ def c5_leg(device, steps=8, parity=True, threads=16, host_threads=1):
     dc = {k: torch.from_numpy(np.ascontiguousarray(getattr(cols, k)).view(
         np.int64 if getattr(cols, k).dtype.itemsize == 8 else np.int32)).to(dev) for k in names}
     doff = torch.from_numpy(cols.offsets.view(np.int64)).to(dev)
-    ptrs = {k: v.data_ptr() for k, v in dc.items()}
+    # each context reads its own copy of the batch (2.9 GB each)
+    dc2 = {k: v.clone() for k, v in dc.items()}
+    doff2 = doff.clone()
+    bufs = [({k: v.data_ptr() for k, v in dc.items()}, doff), ({k: v.data_ptr() for k, v in dc2.items()}, doff2)]
     # two contexts, two steps in flight: step k's link list crosses PCIe (zdl_link_start) while
     # step k + 1's put runs; every step resets, links every span and reads every link back
     ctxs = [N.Context(S, device=device, timing_all=True) for _ in range(2)]
 
     def put(c):
+        bp, bo = bufs[0 if c is ctxs[0] else 1]
         c.reset()
-        c.put_spans_device(ptrs, cols.n_spans, doff.data_ptr(), cols.n_traces)
+        c.put_spans_device(bp, cols.n_spans, bo.data_ptr(), cols.n_traces)
         c.link_start()
 
     for c in ctxs:  # warm (allocations)
@@ -339,7 +371,7 @@ def c5_leg(device, steps=8, parity=True, threads=16, host_threads=1):
            "sparse_merge": k.sparse_ms, "link_compact": k.compact_ms}]
     for c in ctxs:
         c.close()
-    del dc, doff
+    del dc, doff, dc2, doff2, bufs
     gmin = int(os.environ.get("ZDL_GIANT_MIN", "2048")) or None
     gmin = max(gmin, 192) if gmin else None
     big = sizes > 192
@@ -537,6 +569,7 @@ def main():
     ap.add_argument("--no-json", action="store_true", help="skip the JSON v2 ingest side leg")
     ap.add_argument("--no-store", action="store_true", help="skip the resident-store getDependencies side leg")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 (high-cardinality) side leg")
+    ap.add_argument("--no-put-trace", action="store_true", help="skip the per-trace putTrace loop side leg")
     ap.add_argument("--c5-host-threads", type=int, default=1, choices=(1, 2),
                     help="C5 leg: one host thread per context (2) or one alternating both (1)")
     ap.add_argument("--no-traffic", action="store_true",
@@ -591,6 +624,19 @@ def main():
     doff = torch.from_numpy(cols.offsets.view(np.int64)).to(dev)
     ptrs = {k: v.data_ptr() for k, v in dcols.items()}
     ptrs["timestamp"] = None
+    inflight = args.inflight or (2 if world == 1 else 1)
+    # every in-flight context links its OWN copy of the batch (C2: 448 MB each), so a second
+    # reader of the same bytes cannot be served from the 256 MiB Infinity Cache; the
+    # shared-input step is measured beside it (config.ms_per_step_shared_input)
+    batches = [(ptrs, doff)]
+    keep = [dcols]
+    for _ in range(inflight - 1):
+        dc2 = {k: v.clone() for k, v in dcols.items()}
+        keep.append(dc2)
+        p2 = {k: v.data_ptr() for k, v in dc2.items()}
+        p2["timestamp"] = None
+        batches.append((p2, doff.clone()))
+        keep.append(batches[-1][1])
     torch.cuda.synchronize(dev)
 
     # HIP events around k_link on every 8th put of the timed region (each event pair costs
@@ -613,19 +659,20 @@ def main():
     # enqueued before step k's links are read, so the host's work of reading one step's links
     # and launching the next overlaps the GPU's work instead of idling it (~25 us a step at C2).
     # Every step still resets, links every span and reads every link back.
-    inflight = args.inflight or (2 if world == 1 else 1)
     ctxs = [ctx] + [N.Context(S, device=local, timing=True, timing_stride=args.timing_stride)
                     for _ in range(inflight - 1)]
 
-    def launch(c):
+    def launch(c, j=0):
+        bp, bo = batches[j]
         c.reset()
-        c.put_spans_device(ptrs, cols.n_spans, doff.data_ptr(), cols.n_traces)
+        c.put_spans_device(bp, cols.n_spans, bo.data_ptr(), cols.n_traces)
 
-    def run(k_steps):
-        """k_steps steps: every step's put is launched, every step's links are read."""
+    def run(k_steps, shared=False):
+        """k_steps steps: every step's put is launched, every step's links are read. Context j
+        reads batch copy j (shared: every context reads copy 0)."""
         res = None
         for k in range(k_steps):
-            launch(ctxs[k % inflight])
+            launch(ctxs[k % inflight], 0 if shared else k % inflight)
             if k >= inflight - 1:
                 res = ctxs[(k - inflight + 1) % inflight].link(copy=False)
         for k in range(max(k_steps - inflight + 1, 0), k_steps):
@@ -649,27 +696,47 @@ def main():
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
-    # HIP events around every timed put's k_link (a ring per context), averaged once here
+    # HIP events around every timed put's k_link (a ring per context), averaged once here:
+    # with steps in flight two launches overlap, so this is NOT a kernel duration (reported as
+    # kernel_ms.k_link_inflight_events, never priced)
     kts = [float(c.kernel_times().tiles_ms) for c in ctxs]
     kts = [x for x in kts if x > 0] or [float("nan")]
-    tiles = float(np.mean(kts))
-    serial_ms = None
-    if inflight > 1:  # the same steps one at a time (reported beside `value`, not as it)
-        ns = min(args.steps, 10)
+    tiles_inflight = float(np.mean(kts))
+    shared_ms = None
+    if inflight > 1:  # the same in-flight steps with every context reading ONE copy of the batch
         sync_all()
         t1 = time.perf_counter()
-        for _ in range(ns):
-            launch(ctx)
-            ctx.link()
+        run(args.steps, shared=True)
         sync_all()
-        serial_ms = (time.perf_counter() - t1) / ns * 1e3
-    # The step's contexts are done: close them before the side legs. Each context owns a HIP
-    # stream, and with GPU_MAX_HW_QUEUES=4 (the box's setting) streams beyond four share hardware
-    # queues - the C5 leg's two contexts then ran one after the other (7.7 ms a step instead of
-    # 6.1 with its two streams on queues of their own).
+        shared_ms = (time.perf_counter() - t1) / args.steps * 1e3
+    # The step's contexts are done: close them before the serial leg and the side legs. Each
+    # context owns a HIP stream, and with GPU_MAX_HW_QUEUES=4 (the box's setting) streams beyond
+    # four share hardware queues - the C5 leg's two contexts then ran one after the other (7.7 ms
+    # a step instead of 6.1 with its two streams on queues of their own).
     for c in ctxs:
         c.close()
+    # The serial leg: the same step one at a time on a context timing EVERY k_link (HIP events
+    # on its stream, nothing else on the GPU) - this k_link duration prices `roofline`
+    sctx = N.Context(S, device=local, timing=True, timing_stride=1) if world == 1 else None
+    serial_ms = None
+    tiles = tiles_inflight
+    if sctx is not None:
+        ns = max(min(args.steps, 20), 3)
+        for _ in range(2):
+            launch(sctx)
+            sctx.link()
+        sctx.sync()
+        sctx.kernel_times()
+        t1 = time.perf_counter()
+        for _ in range(ns):
+            launch(sctx)
+            sctx.link(copy=False)
+        sctx.sync()
+        serial_ms = (time.perf_counter() - t1) / ns * 1e3
+        tiles = float(sctx.kernel_times().tiles_ms)
+        sctx.close()
     ctxs = []
+    del keep, batches[1:]
     if dist:
         tt = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -741,6 +808,11 @@ def main():
         h2d = h2d_leg(cols, S, local)
         log(f"host buffers: H2D {h2d['h2d_ms']:.2f} ms ({h2d['h2d_gbs']:.1f} GB/s pinned), put+link from pageable "
             f"host columns {h2d['e2e_ms']:.2f} ms")
+    ptl = None
+    if side and not args.no_put_trace:
+        ptl = put_trace_leg(cols, S, local, (p, c, n, e))
+        log(f"putTrace loop: {ptl['ms']:.1f} ms for {ptl['calls']} calls ({ptl['spans_per_s']:.3e} spans/s, "
+            f"{ptl['us_per_call']:.3f} us/call), links {ptl['parity']}")
     c5 = None
     if side and not args.no_c5:
         c5 = c5_leg(local, parity=not args.no_parity, threads=cpu_info()["usable"], host_threads=args.c5_host_threads)
@@ -810,12 +882,17 @@ def main():
             "config": {"workload": w.name, "spans_per_gpu": cols.n_spans, "traces_per_gpu": cols.n_traces,
                        "services": S, "parallelism": f"trace-shard x{world}", "combine": combine,
                        "inflight": inflight, "ms_per_step_serial": serial_ms,
-                       "kernel_ms": {"k_link": tiles},
+                       "ms_per_step_shared_input": shared_ms,
+                       "kernel_ms": {"k_link": tiles,
+                                     "k_link_source": "HIP events around every k_link of the serial leg (one "
+                                                      "step at a time, nothing else on the GPU)" if world == 1
+                                     else "HIP events around every 8th k_link (one step in flight)",
+                                     "k_link_inflight_events": tiles_inflight},
                        "step_roofline_frac": bytes_launch / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
                        "k_link_read_frac": read_launch / (tiles * 1e-3) / 1e9 / HBM_PEAK_GBS,
                        "parity": parity, "links": int(len(p)), "insertion_order": ins, "host_buffers": h2d,
                        "proto3_ingest": p3, "json_v2_ingest": jleg, "store_get_dependencies": sleg,
-                       "mysql_rows": rows_leg, "c5": c5},
+                       "mysql_rows": rows_leg, "put_trace_loop": ptl, "c5": c5},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "k_link", "algorithmic_bytes_per_launch": klink_bytes,

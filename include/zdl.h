@@ -36,9 +36,11 @@
 extern "C" {
 #endif
 
-#define ZDL_ABI_VERSION 4  /* 2: zdl_config.n_devices / device_ids, RCCL combine; 3: zdl_kernel_times
+#define ZDL_ABI_VERSION 5  /* 2: zdl_config.n_devices / device_ids, RCCL combine; 3: zdl_kernel_times
                               per phase of a put (mid_ms, giant_ms, sparse_ms); 4: trace id widths
-                              (zdl_store_append_ids, zdl_decoded.dev_trace_wide) */
+                              (zdl_store_append_ids, zdl_decoded.dev_trace_wide); 5: zdl_put_trace,
+                              a trace whose Trace.merge throws adds nothing, a started link locks
+                              the context until zdl_link_finish */
 
 /* ---- status codes ---- */
 #define ZDL_OK          0
@@ -202,9 +204,29 @@ int zdl_put_spans(zdl_ctx* ctx, const zdl_span_cols* cols, uint64_t n_spans,
                   const uint64_t* trace_offsets, uint64_t n_traces);
 
 /* Same, with every pointer (columns and offsets) in device memory of the context's
- * device. Asynchronous on the context stream; errors surface at zdl_sync/zdl_link. */
+ * device. Asynchronous on the context stream; errors surface at zdl_sync/zdl_link.
+ * Lifetime: the put may still read the columns and offsets after this call returns - on a
+ * small dense table its last kernels (k_mid / k_tail, only when some trace needs them) are
+ * launched at the context's NEXT call (zdl_sync, zdl_link, zdl_link_start, zdl_reset, a put,
+ * zdl_table_export, zdl_destroy). Keep them valid and unchanged until one of those has
+ * returned; a device-wide synchronize (hipDeviceSynchronize) does not complete the put. */
 int zdl_put_spans_device(zdl_ctx* ctx, const zdl_span_cols* dev_cols, uint64_t n_spans,
                          const uint64_t* dev_trace_offsets, uint64_t n_traces);
+
+/* DependencyLinker.putTrace (internal/DependencyLinker.java:53) called once per trace, as the
+ * reference's callers loop (storage/InMemoryStorage.java:340; mysql-v1
+ * AggregateDependencies.java:81): `cols` holds ONE trace's n_spans spans (host memory, read
+ * during the call only; trace_lo needed by device groups, timestamp when a window or days are
+ * set). The trace is appended to a pinned staging batch that is put as one launch when it
+ * fills (ZDL_STAGE_SPANS, default 2^20 spans) or when the context is next used for anything
+ * else (zdl_link, zdl_sync, another put, a setting...), so traces are linked in call order.
+ * A trace with two spans of one (id, shared) - the only input on which Trace.merge can throw -
+ * is put alone and waited for: ZDL_EREF_NPE is returned by THIS call (quirk Q1), the trace adds
+ * nothing, and the context stays usable, as the Java linker does after a caught throw. Errors
+ * of a staged batch (ZDL_EINVAL: a service id >= n_services) are returned by the call that
+ * flushes it or by the next zdl_sync / zdl_link. n_spans = 0 is a no-op (putTrace of an empty
+ * list). zdl_reset drops staged traces with the counts. */
+int zdl_put_trace(zdl_ctx* ctx, const zdl_span_cols* cols, uint64_t n_spans);
 
 /* ---- device-resident span store (the ingest side of InMemoryStorage,
  * storage/InMemoryStorage.java:156-181 accept) ----

@@ -278,3 +278,50 @@ def test_decoded_ingest_strict_no_arg_get_dependencies(fmt, seed):
             break
         assert _as_list(store.get_dependencies()) == want
     store.close()
+
+
+def _npe_trace(tid, ts):
+    """A trace on which DependencyLinker.putTrace throws (quirk Q1), found by the oracle."""
+    r = random.Random(11)
+    for _ in range(20000):
+        t = [s.to_builder(trace_id=tid, timestamp=ts) for s in random_trace(r, n=r.randint(2, 8))]
+        try:
+            O.DependencyLinker().put_trace(t)
+        except O.ReferenceNPE:
+            return t
+    raise AssertionError("no NPE trace found")
+
+
+def test_query_context_growth_drops_stale_npe():
+    """a query that raised NPE leaves its context's status word set; when the
+    service dictionary then grows past that context's capacity, the next query must get a
+    fresh context (not link() the poisoned one) and answer like the oracle."""
+    store = InMemoryStorage()
+    ref = O.InMemoryStorage()
+    old = _npe_trace("00000000000000a1", BASE_US)
+    store.accept(old).execute()
+    ref.accept(old)
+    day = 86_400_000
+    end1 = BASE_US // 1000 + 1000
+    with pytest.raises(N.ReferenceNullPointerException):
+        store.get_dependencies(end1, day).execute()
+    # 90 new services (past the dense capacity of 67), a day later: outside the old trace's window
+    ts2 = BASE_US + 2 * day * 1000
+    new = []
+    for k in range(90):
+        tid = format(0x1000 + k, "016x")
+        new += [Span_(tid, "01", None, "SERVER", f"svc{k}"), Span_(tid, "02", "01", "CLIENT", f"svc{k}", f"svc{k + 1}")]
+    new = [s.to_builder(timestamp=ts2) for s in new]
+    store.accept(new).execute()
+    ref.accept(new)
+    end2 = ts2 // 1000 + 1000
+    want = _as_list(ref.get_dependencies(end2, day))
+    assert len(want) == 90
+    assert _as_list(store.get_dependencies(end2, day).execute()) == want
+    store.close()
+
+
+def Span_(tid, sid, pid, kind, svc, remote=None):
+    from zipkin_amd.model import Endpoint, Kind, Span
+    return Span.create(tid, sid, pid, getattr(Kind, kind), local_endpoint=Endpoint.create(svc, None, 0),
+                       remote_endpoint=Endpoint.create(remote, None, 0) if remote else None)

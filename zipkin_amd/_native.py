@@ -49,9 +49,9 @@ EXPORTS = (
     "zdl_decoder_download", "zdl_decoder_kernel_ms", "zdl_put_mysql_rows", "zdl_rows_last_error",
     "zdl_comm_unique_id", "zdl_comm_init", "zdl_put_spans_device_multi", "zdl_device_count", "zdl_shard_of",
     "zdl_tree_export", "zdl_tree_reasons", "zdl_decode_json_v2", "zdl_decode_retry", "zdl_decoder_struct_ms", "zdl_decoder_exact_spans",
-    "zdl_link_start", "zdl_link_finish",
+    "zdl_link_start", "zdl_link_finish", "zdl_put_trace",
 )
-ZDL_ABI_VERSION = 4
+ZDL_ABI_VERSION = 5
 ZDL_COMM_ID_BYTES = 128
 
 
@@ -140,6 +140,7 @@ def lib() -> C.CDLL:
     L.zdl_set_window.argtypes = [vp, i64, i64]
     L.zdl_put_spans.argtypes = [vp, C.POINTER(SpanCols), u64, vp, u64]
     L.zdl_put_spans_device.argtypes = [vp, C.POINTER(SpanCols), u64, vp, u64]
+    L.zdl_put_trace.argtypes = [vp, C.POINTER(SpanCols), u64]
     L.zdl_sync.argtypes = [vp]
     L.zdl_link.argtypes = [vp, C.c_int, C.POINTER(Links)]
     L.zdl_link_start.argtypes = [vp, C.c_int]
@@ -339,6 +340,14 @@ class Context:
         sc = SpanCols(None, _ptr(cols.id), _ptr(cols.parent_id), _ptr(cols.local_svc), _ptr(cols.remote_svc),
                       _ptr(cols.local_ip4), _ptr(cols.local_ip6), _ptr(cols.port_flags), _ptr(cols.timestamp))
         self.check(self._L.zdl_put_spans(self.h, C.byref(sc), cols.n_spans, _ptr(cols.offsets), cols.n_traces))
+
+    def put_trace(self, cols) -> None:
+        """zdl_put_trace: ONE trace's host columns (columnar.Columns with one trace), staged;
+        raises ReferenceNullPointerException from this call when its Trace.merge throws."""
+        sc = SpanCols(_ptr(cols.trace_lo), _ptr(cols.id), _ptr(cols.parent_id), _ptr(cols.local_svc),
+                      _ptr(cols.remote_svc), _ptr(cols.local_ip4), _ptr(cols.local_ip6), _ptr(cols.port_flags),
+                      _ptr(cols.timestamp))
+        self.check(self._L.zdl_put_trace(self.h, C.byref(sc), cols.n_spans))
 
     def put_spans_ungrouped(self, cols, ord=None) -> None:
         """Host columns in any trace order (cols.trace_lo read, cols.offsets ignored): the
@@ -552,6 +561,7 @@ class Decoder:
             raise ZdlError(ZDL_EDEVICE, "zdl_decoder_create failed")
         self.h = C.c_void_p(h)
         self._L = L
+        self.gen = 0  # decodes so far: a batch's device columns belong to one generation
 
     def check(self, rc: int):
         if rc == ZDL_OK:
@@ -563,11 +573,13 @@ class Decoder:
 
     def decode(self, data: bytes) -> Decoded:
         out = Decoded()
+        self.gen += 1
         self.check(self._L.zdl_decode_proto3(self.h, bytes(data), len(data), C.byref(out)))
         return out
 
     def decode_json(self, data: bytes) -> Decoded:
         out = Decoded()
+        self.gen += 1
         self.check(self._L.zdl_decode_json_v2(self.h, bytes(data), len(data), C.byref(out)))
         return out
 

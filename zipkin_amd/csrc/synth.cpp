@@ -539,3 +539,37 @@ extern "C" uint64_t zdl_synth_json_v2(uint64_t n, const uint64_t* trace_lo, cons
   w.str("]");
   return w.pos;
 }
+
+#include "../../include/zdl.h"
+
+extern "C" {
+
+// The caller side of zdl_put_trace as the reference's callers drive putTrace - one call per
+// trace, in order (InMemoryStorage.java:340 linkDependencies, mysql-v1
+// AggregateDependencies.java:81) - what a JNI shim does after packing each trace: the column
+// slices of trace t are handed over, nothing else. `put` is zdl_put_trace (passed in so this
+// host helper does not link libzdl). Returns the first non-zero status (and its trace in *at).
+int zdl_synth_put_trace_loop(int (*put)(zdl_ctx*, const zdl_span_cols*, uint64_t), zdl_ctx* ctx,
+                             const zdl_span_cols* cols, const uint64_t* off, uint64_t n_traces, uint64_t* at) {
+  for (uint64_t t = 0; t < n_traces; ++t) {
+    const uint64_t b = off[t];
+    zdl_span_cols c{};
+    c.trace_lo = cols->trace_lo ? cols->trace_lo + b : nullptr;
+    c.id = cols->id + b;
+    c.parent_id = cols->parent_id + b;
+    c.local_svc = cols->local_svc + b;
+    c.remote_svc = cols->remote_svc + b;
+    c.local_ip4 = cols->local_ip4 + b;
+    c.local_ip6 = cols->local_ip6 + b;
+    c.port_flags = cols->port_flags + b;
+    c.timestamp = cols->timestamp ? cols->timestamp + b : nullptr;
+    const int rc = put(ctx, &c, off[t + 1] - b);
+    if (rc != 0) {
+      if (at) *at = t;
+      return rc;
+    }
+  }
+  return 0;
+}
+
+}  // extern "C"

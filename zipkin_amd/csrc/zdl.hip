@@ -944,7 +944,10 @@ __device__ __forceinline__ void big_exact(const Args& A, uint64_t b, int n, uint
     npe |= merge_group(v, p, ge);
   }
   if (npe) atomicOr(A.status, ST_NPE);
-  big_sync();
+  if (__syncthreads_or(npe ? 1 : 0)) {  // Trace.merge threw: putTrace adds nothing for the trace
+    if (A.sparse && threadIdx.x == 0) A.tseg_big[bi] = 0;
+    return;
+  }
   for (int p = threadIdx.x; p < n; p += BIG_WG) {
     const uint32_t s = v.perm[p];
     if (v.live[p] && !is_shared(v.pf[s]) && v.pid[s] == 0) atomicMin(&sh_root, p);
@@ -1452,6 +1455,26 @@ struct DevBuf {
   }
 };
 
+// zdl_put_trace's host staging: the traces of consecutive putTrace calls packed as one CSR
+// batch in pinned memory (two slots: one filling while the other's upload runs), put as one
+// launch when a slot fills or the context is used otherwise (zdl_stage.inc)
+struct StageSlot {
+  unsigned char* mem = nullptr;  // one pinned block: the columns, then the offsets
+  uint64_t *lo = nullptr, *id = nullptr, *pid = nullptr, *off = nullptr;
+  int32_t *ls = nullptr, *rs = nullptr, *i4 = nullptr, *i6 = nullptr;
+  uint32_t* pf = nullptr;
+  int64_t* ts = nullptr;
+  uint64_t n = 0, nt = 0;        // spans and traces staged
+  bool has_lo = false, has_ts = false;
+  hipEvent_t done = nullptr;     // recorded after the slot's uploads
+  bool inflight = false;
+};
+struct Stage {
+  StageSlot slot[2];
+  int cur = 0;
+  uint64_t cap = 0;  // spans (and traces) per slot
+};
+
 }  // namespace
 
 struct zdl_ctx {
@@ -1600,6 +1623,7 @@ struct zdl_ctx {
   int lazy_wmode = 0, lazy_dense = 0;
   int link_pending = -1;  // zdl_link_start's order until zdl_link_finish (-1: none)
   bool link_async = false;  // the started link is a sparse compaction in flight
+  Stage stg;                // zdl_put_trace's staged traces
 };
 
 namespace {
@@ -1696,6 +1720,9 @@ int group_first(zdl_ctx* g, int rc, zdl_ctx* s = nullptr) {
 int group_put(zdl_ctx* g, const zdl_span_cols* col, uint64_t n_spans, const uint64_t* off, uint64_t n_traces);
 int group_export(zdl_ctx* g, void* dev_call, void* dev_err);
 static int resolve_lazy(zdl_ctx* c, bool wait);  // a lazy put's k_mid / k_tail (below)
+static int stage_flush(zdl_ctx* c);                // zdl_put_trace's staged traces as one put
+static void stage_drop(zdl_ctx* c);                // ... discarded (zdl_reset)
+static void stage_free(zdl_ctx* c);
 
 // splitmix64 finaliser (shard.py's): trace t goes to device splitmix64(trace_lo) % n
 inline uint64_t splitmix64(uint64_t x) {
@@ -1843,12 +1870,14 @@ void zdl_destroy(zdl_ctx* c) {
     for (auto& cm : c->comms)
       if (cm) (void)ncclCommDestroy(cm);
     for (auto* s : c->sub) zdl_destroy(s);
+    stage_free(c);
     delete c;
     return;
   }
   if (c->comm) (void)ncclCommDestroy(c->comm);
   (void)hipSetDevice(c->device);
   (void)resolve_lazy(c, false);
+  stage_free(c);
   c->red_call.release();
   c->red_err.release();
   (void)hipSetDevice(c->device);
@@ -1941,6 +1970,8 @@ void* zdl_stream(zdl_ctx* c) {
 
 int zdl_set_ranks(zdl_ctx* c, int dict, const int32_t* rank, uint32_t n) {
   if (!c || dict < 0 || dict > 2) return fail(c, ZDL_EINVAL, "bad dictionary");
+  if (c->link_pending >= 0) return fail(c, ZDL_EINVAL, "zdl_set_ranks: a started link is not finished (zdl_link_finish)");
+  if (const int frc = stage_flush(c)) return frc;  // staged putTrace calls come first
   if (!c->sub.empty()) return group_each(c, [&](zdl_ctx* s) { return zdl_set_ranks(s, dict, rank, n); });
   HIP_TRY(c, enter(c));
   c->host_rank[dict].assign(rank, rank + n);
@@ -1957,6 +1988,8 @@ int zdl_set_ranks(zdl_ctx* c, int dict, const int32_t* rank, uint32_t n) {
 
 int zdl_set_days(zdl_ctx* c, int64_t day0_ms, uint32_t n_days) {
   if (!c) return ZDL_EINVAL;
+  if (c->link_pending >= 0) return fail(c, ZDL_EINVAL, "zdl_set_days: a started link is not finished (zdl_link_finish)");
+  if (const int frc = stage_flush(c)) return frc;  // staged putTrace calls come first
   if (!c->sub.empty() || c->comm) return fail(c, ZDL_EINVAL, "zdl_set_days: one device, one process");
   if (c->sparse) return fail(c, ZDL_EINVAL, "zdl_set_days: needs the S x S table (a sparse context has none)");
   if (n_days > 255) return fail(c, ZDL_EINVAL, "zdl_set_days: at most 255 days");
@@ -1980,6 +2013,8 @@ int zdl_set_days(zdl_ctx* c, int64_t day0_ms, uint32_t n_days) {
 
 int zdl_set_window(zdl_ctx* c, int64_t end_ts_ms, int64_t lookback_ms) {
   if (!c) return ZDL_EINVAL;
+  if (c->link_pending >= 0) return fail(c, ZDL_EINVAL, "zdl_set_window: a started link is not finished (zdl_link_finish)");
+  if (const int frc = stage_flush(c)) return frc;  // staged putTrace calls come first
   if (!c->sub.empty()) return group_each(c, [&](zdl_ctx* s) { return zdl_set_window(s, end_ts_ms, lookback_ms); });
   if (c->days && lookback_ms > 0) return fail(c, ZDL_EINVAL, "zdl_set_window: not with daily buckets");
   if (lookback_ms <= 0) {
@@ -2127,6 +2162,10 @@ static int giant_run(zdl_ctx* c, Args& A, uint64_t n_spans, uint64_t n_traces) {
   const uint32_t nl = c->h_gmeta[0];
   if (nl == 0) return ZDL_OK;
   if (nl > n_traces) return fail(c, ZDL_EDEVICE, "giant tier: inconsistent big-trace count");
+  // k_g_mark packs the giant and rest counts in 20 bits each of one scan word: a back list of
+  // 2^20 traces or more would carry into the next field, so the tier stands aside and k_tail
+  // takes the whole back list (A.grest stays null)
+  if (nl >= GMARK_MAX) return ZDL_OK;
   const uint64_t ntmax = n_spans / GT + nl + 1;
   HIP_TRY(c, c->gg_bi.ensure(nl));
   HIP_TRY(c, c->gg_n.ensure(nl));
@@ -2928,6 +2967,8 @@ int zdl_store_selection(const zdl_store* cst, uint32_t* perm, uint64_t* trace_of
 
 int zdl_put_selection(zdl_ctx* c, const zdl_store* st) {
   if (!c || !st) return fail(c, ZDL_EINVAL, "null argument");
+  if (c->link_pending >= 0) return fail(c, ZDL_EINVAL, "zdl_put_selection: a started link is not finished (zdl_link_finish)");
+  if (const int frc = stage_flush(c)) return frc;  // staged putTrace calls come first
   if (!c->sub.empty()) return fail(c, ZDL_EINVAL, "zdl_put_selection: a store lives on one device");
   if (st->device != c->device) return fail(c, ZDL_EINVAL, "zdl_put_selection: store and context on different devices");
   if (!st->sel_valid) return fail(c, ZDL_EINVAL, "zdl_put_selection: no current selection (zdl_store_select)");
@@ -2940,6 +2981,8 @@ int zdl_put_selection(zdl_ctx* c, const zdl_store* st) {
 int zdl_put_stored(zdl_ctx* c, const zdl_store* st, const uint32_t* perm, uint64_t n_sel, const uint64_t* off,
                    uint64_t n_traces) {
   if (!c || !st || (n_sel && !perm) || !off) return fail(c, ZDL_EINVAL, "null argument");
+  if (c->link_pending >= 0) return fail(c, ZDL_EINVAL, "zdl_put_stored: a started link is not finished (zdl_link_finish)");
+  if (const int frc = stage_flush(c)) return frc;  // staged putTrace calls come first
   if (!c->sub.empty()) return fail(c, ZDL_EINVAL, "zdl_put_stored: a store lives on one device");
   if (st->device != c->device) return fail(c, ZDL_EINVAL, "zdl_put_stored: store and context on different devices");
   if (n_traces == 0 || n_sel == 0) return ZDL_OK;
@@ -2960,6 +3003,8 @@ int zdl_put_stored(zdl_ctx* c, const zdl_store* st, const uint32_t* perm, uint64
 int zdl_put_spans_device(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans, const uint64_t* off,
                          uint64_t n_traces) {
   if (!c || !col) return fail(c, ZDL_EINVAL, "null argument");
+  if (c->link_pending >= 0) return fail(c, ZDL_EINVAL, "zdl_put_spans_device: a started link is not finished (zdl_link_finish)");
+  if (const int frc = stage_flush(c)) return frc;  // staged putTrace calls come first
   if (!c->sub.empty())
     return fail(c, ZDL_EINVAL, "zdl_put_spans_device: a device group takes zdl_put_spans or zdl_put_spans_device_multi");
   if (n_spans == 0 || (off && n_traces == 0)) return ZDL_OK;
@@ -2976,6 +3021,8 @@ int zdl_put_spans_device(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans,
 
 int zdl_sync(zdl_ctx* c) {
   if (!c) return ZDL_EINVAL;
+  if (c->link_pending < 0)
+    if (const int frc = stage_flush(c)) return frc;
   if (!c->sub.empty()) return group_each(c, [&](zdl_ctx* s) { return zdl_sync(s); });
   HIP_TRY(c, enter(c));
   {
@@ -2992,6 +3039,8 @@ int zdl_sync(zdl_ctx* c) {
 int zdl_put_spans(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans, const uint64_t* off,
                   uint64_t n_traces) {
   if (!c || !col) return fail(c, ZDL_EINVAL, "null argument");
+  if (c->link_pending >= 0) return fail(c, ZDL_EINVAL, "zdl_put_spans: a started link is not finished (zdl_link_finish)");
+  if (const int frc = stage_flush(c)) return frc;  // staged putTrace calls come first
   if (!c->sub.empty()) return group_put(c, col, n_spans, off, n_traces);
   if (off) {
     if (n_traces == 0) return ZDL_OK;
@@ -3052,6 +3101,8 @@ int zdl_put_spans(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans, const 
 
 int zdl_reset(zdl_ctx* c) {
   if (!c) return ZDL_EINVAL;
+  if (c->link_pending >= 0) return fail(c, ZDL_EINVAL, "zdl_reset: a started link is not finished (zdl_link_finish)");
+  stage_drop(c);  // traces staged by zdl_put_trace before the reset are dropped with the counts
   if (!c->sub.empty()) return group_each(c, [&](zdl_ctx* s) { return zdl_reset(s); });
   HIP_TRY(c, enter(c));
   {
@@ -3363,6 +3414,8 @@ extern "C" {
 
 int zdl_link(zdl_ctx* c, int order, zdl_links* out) {
   if (!c || !out) return ZDL_EINVAL;
+  if (c->link_pending >= 0) return fail(c, ZDL_EINVAL, "zdl_link: a started link is not finished (zdl_link_finish)");
+  if (const int frc = stage_flush(c)) return frc;  // staged putTrace calls come first
   if (!c->sub.empty()) return group_link(c, order, out);
   if (c->lazy_pending) {
     HIP_TRY(c, enter(c));
@@ -3395,6 +3448,7 @@ int zdl_link(zdl_ctx* c, int order, zdl_links* out) {
 int zdl_link_start(zdl_ctx* c, int order) {
   if (!c) return ZDL_EINVAL;
   if (c->link_pending >= 0) return fail(c, ZDL_EINVAL, "zdl_link_start: a started link is not finished");
+  if (const int frc = stage_flush(c)) return frc;
   c->link_pending = order;
   c->link_async = false;
   if (c->sparse && !c->comm && c->sub.empty() && order == ZDL_ORDER_SORTED && !c->poisoned) {
@@ -3427,6 +3481,8 @@ int zdl_link_finish(zdl_ctx* c, zdl_links* out) {
 // ITDependencies.aggregateLinks' map of per-day DependencyLinker.link() lists.
 int zdl_link_days(zdl_ctx* c, int order, zdl_day_links* out) {
   if (!c || !out) return ZDL_EINVAL;
+  if (c->link_pending >= 0) return fail(c, ZDL_EINVAL, "zdl_link_days: a started link is not finished (zdl_link_finish)");
+  if (const int frc = stage_flush(c)) return frc;  // staged putTrace calls come first
   if (!c->sub.empty() || c->comm) return fail(c, ZDL_EINVAL, "zdl_link_days: one device, one process");
   if (!c->days) return fail(c, ZDL_EINVAL, "zdl_link_days: no daily buckets (zdl_set_days)");
   if (order == ZDL_ORDER_INSERTION && !c->ord)
@@ -3531,6 +3587,8 @@ int zdl_link_days(zdl_ctx* c, int order, zdl_day_links* out) {
 int zdl_merge_links(zdl_ctx* c, const int32_t* parent, const int32_t* child, const int64_t* call_count,
                     const int64_t* error_count, uint64_t n, zdl_links* out) {
   if (!c || !out) return ZDL_EINVAL;
+  if (c->link_pending >= 0) return fail(c, ZDL_EINVAL, "zdl_merge_links: a started link is not finished (zdl_link_finish)");
+  if (const int frc = stage_flush(c)) return frc;  // staged putTrace calls come first
   if (!c->sub.empty()) return group_first(c, zdl_merge_links(c->sub[0], parent, child, call_count, error_count, n, out));
   HIP_TRY(c, enter(c));
   const uint64_t SS = (uint64_t)c->S * c->S;
@@ -3607,6 +3665,8 @@ int zdl_merge_links(zdl_ctx* c, const int32_t* parent, const int32_t* child, con
 int zdl_add_links(zdl_ctx* c, const int32_t* parent, const int32_t* child, const int64_t* call_count,
                   const int64_t* error_count, uint64_t n) {
   if (!c) return ZDL_EINVAL;
+  if (c->link_pending >= 0) return fail(c, ZDL_EINVAL, "zdl_add_links: a started link is not finished (zdl_link_finish)");
+  if (const int frc = stage_flush(c)) return frc;  // staged putTrace calls come first
   if (!c->sub.empty()) return group_first(c, zdl_add_links(c->sub[0], parent, child, call_count, error_count, n));
   if (c->days) return fail(c, ZDL_EINVAL, "zdl_add_links: not with daily buckets");
   if (n == 0) return ZDL_OK;
@@ -3656,6 +3716,8 @@ int zdl_add_links(zdl_ctx* c, const int32_t* parent, const int32_t* child, const
 
 int zdl_table_export(zdl_ctx* c, void* dev_call, void* dev_err) {
   if (!c || !dev_call || !dev_err) return ZDL_EINVAL;
+  if (c->link_pending >= 0) return fail(c, ZDL_EINVAL, "zdl_table_export: a started link is not finished (zdl_link_finish)");
+  if (const int frc = stage_flush(c)) return frc;  // staged putTrace calls come first
   if (!c->sub.empty()) return group_export(c, dev_call, dev_err);
   if (c->sparse) return fail(c, ZDL_EINVAL, "zdl_table_export: a sparse context has no S x S table");
   HIP_TRY(c, enter(c));
@@ -3679,6 +3741,8 @@ int zdl_table_export(zdl_ctx* c, void* dev_call, void* dev_err) {
 
 int zdl_table_import(zdl_ctx* c, const void* dev_call, const void* dev_err) {
   if (!c || !dev_call || !dev_err) return ZDL_EINVAL;
+  if (c->link_pending >= 0) return fail(c, ZDL_EINVAL, "zdl_table_import: a started link is not finished (zdl_link_finish)");
+  if (const int frc = stage_flush(c)) return frc;  // staged putTrace calls come first
   if (!c->sub.empty()) {  // the first device holds the imported counts, the others none
     for (size_t d = 1; d < c->sub.size(); ++d) {
       const int rc = zdl_reset(c->sub[d]);
@@ -4022,6 +4086,8 @@ int zdl_comm_unique_id(uint8_t* out) {
 
 int zdl_comm_init(zdl_ctx* c, const uint8_t* id, int rank, int world) {
   if (!c || !id || world < 1 || rank < 0 || rank >= world) return fail(c, ZDL_EINVAL, "zdl_comm_init: bad rank / world");
+  if (c->link_pending >= 0) return fail(c, ZDL_EINVAL, "zdl_comm_init: a started link is not finished (zdl_link_finish)");
+  if (const int frc = stage_flush(c)) return frc;  // staged putTrace calls come first
   if (!c->sub.empty()) return fail(c, ZDL_EINVAL, "zdl_comm_init: a device group has its own communicator");
   if (c->ord || c->days) return fail(c, ZDL_EINVAL, "zdl_comm_init: insertion order and daily buckets are per process");
   if (c->comm) return fail(c, ZDL_EINVAL, "zdl_comm_init: already joined");
@@ -4041,6 +4107,8 @@ int zdl_comm_init(zdl_ctx* c, const uint8_t* id, int rank, int world) {
 int zdl_put_spans_device_multi(zdl_ctx* c, const zdl_span_cols* cols, const uint64_t* n_spans,
                                const uint64_t* const* offsets, const uint64_t* n_traces) {
   if (!c || !cols || !n_spans || !offsets || !n_traces) return fail(c, ZDL_EINVAL, "null argument");
+  if (c->link_pending >= 0) return fail(c, ZDL_EINVAL, "zdl_put_spans_device_multi: a started link is not finished (zdl_link_finish)");
+  if (const int frc = stage_flush(c)) return frc;  // staged putTrace calls come first
   if (c->sub.empty()) return zdl_put_spans_device(c, &cols[0], n_spans[0], offsets[0], n_traces[0]);
   for (size_t d = 0; d < c->sub.size(); ++d) {
     const int rc = zdl_put_spans_device(c->sub[d], &cols[d], n_spans[d], offsets[d], n_traces[d]);
@@ -4061,6 +4129,8 @@ extern "C" {
 
 int zdl_tree_export(zdl_ctx* c, int32_t* node_of, int32_t* parent, int32_t* bfs, uint64_t n) {
   if (!c || !node_of || !parent || !bfs) return ZDL_EINVAL;
+  if (c->link_pending >= 0) return fail(c, ZDL_EINVAL, "zdl_tree_export: a started link is not finished (zdl_link_finish)");
+  if (const int frc = stage_flush(c)) return frc;  // staged putTrace calls come first
   if (!(c->flags & (ZDL_FLAG_TREE_EXPORT | ZDL_FLAG_TREE_STREAM)) || !c->sub.empty())
     return fail(c, ZDL_EINVAL, "context without ZDL_FLAG_TREE_EXPORT / ZDL_FLAG_TREE_STREAM");
   if (n != c->tr_n) return fail(c, ZDL_EINVAL, "zdl_tree_export: n must be the last put's span count");
@@ -4075,6 +4145,8 @@ int zdl_tree_export(zdl_ctx* c, int32_t* node_of, int32_t* parent, int32_t* bfs,
 
 int zdl_tree_reasons(zdl_ctx* c, uint8_t* reason, int32_t* ancestor, int32_t* link, int32_t* sorted, uint64_t n) {
   if (!c || !reason || !ancestor || !link || !sorted) return ZDL_EINVAL;
+  if (c->link_pending >= 0) return fail(c, ZDL_EINVAL, "zdl_tree_reasons: a started link is not finished (zdl_link_finish)");
+  if (const int frc = stage_flush(c)) return frc;  // staged putTrace calls come first
   if (!(c->flags & (ZDL_FLAG_TREE_EXPORT | ZDL_FLAG_TREE_STREAM)) || !c->sub.empty())
     return fail(c, ZDL_EINVAL, "context without ZDL_FLAG_TREE_EXPORT / ZDL_FLAG_TREE_STREAM");
   if (n != c->tr_n) return fail(c, ZDL_EINVAL, "zdl_tree_reasons: n must be the last put's span count");
@@ -4089,3 +4161,5 @@ int zdl_tree_reasons(zdl_ctx* c, uint8_t* reason, int32_t* ancestor, int32_t* li
 }
 
 }  // extern "C"
+
+#include "zdl_stage.inc"  // zdl_put_trace: putTrace call by call, staged into batches

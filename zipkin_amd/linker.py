@@ -66,8 +66,14 @@ class DependencyLinker:
         self._ranked = (-1, -1, -1)
 
     # -- context management -------------------------------------------------
-    def _context(self, window: bool = False) -> N.Context:
+    def _context(self, window: bool = False, carry: bool = True) -> N.Context:
+        """The engine context sized for the dictionary. carry=False (a query context that is
+        reset before use): a context too small is closed, not linked - its counts and status
+        word (a previous query's NPE or device error included) are dropped with it."""
         need = _capacity(max(len(self.svc), 1), window)
+        if self._ctx is not None and not carry and self._ctx.n_services < need:
+            self._ctx.close()
+            self._ctx = None
         if self._ctx is None:
             self._ctx = N.Context(need, self.device, insertion_order=self.insertion_order, tree_export=self._fine)
             self._ranked = (-1, -1, -1)
@@ -93,10 +99,16 @@ class DependencyLinker:
 
     # -- reference API --------------------------------------------------------
     def put_trace(self, spans: Sequence[Span]) -> "DependencyLinker":
-        """putTrace (DependencyLinker.java:53): spans of one trace."""
+        """putTrace (DependencyLinker.java:53): spans of one trace. Staged by the engine
+        (zdl_put_trace): consecutive calls are linked as one batch launch, in call order; an
+        NPE (quirk Q1) is raised by the call whose trace throws, and the linker stays usable."""
         if not spans:
             return self
-        return self.put_traces([spans])
+        if self._fine:  # the FINE log renders each put's tree: one put per call
+            return self.put_traces([spans])
+        cols = pack_traces([spans], self.svc, self.ip4, self.ip6)
+        self._context().put_trace(cols)
+        return self
 
     def put_traces(self, traces: Sequence[Sequence[Span]]) -> "DependencyLinker":
         """Batch of putTrace calls in one engine launch."""

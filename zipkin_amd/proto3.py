@@ -32,10 +32,18 @@ class DecodedBatch:
     dev_trace_hi: Optional[int] = None  # device pointer: the trace ids' high 64 bits (0 = 64-bit id)
     _dec: Optional[N.Decoder] = None
     dev_trace_wide: Optional[int] = None  # device pointer: the ids' widths (None: 128-bit iff hi != 0)
+    _gen: int = 0  # the decoder's generation that produced these columns
+
+    def __post_init__(self):
+        if self._dec is not None:
+            self._gen = self._dec.gen
 
     def _host(self, name, dtype):
         if self.n_spans == 0:
             return np.zeros(0, dtype)
+        if self._dec.gen != self._gen:
+            raise RuntimeError("DecodedBatch: its decoder has decoded another batch since; the device columns "
+                               "are valid only until the next decode")
         return self._dec.download(self.n_spans, (name,))[name]
 
     @property

@@ -176,10 +176,12 @@ class InMemoryStorage:
             linker = DependencyLinker(self.device, insertion_order=self.insertion_order)
             linker.svc, linker.ip4, linker.ip6 = self._linker.svc, self._linker.ip4, self._linker.ip6
             self._qlinker[key] = linker
-        fresh = linker._ctx is None
-        ctx = linker._context(key)
-        if not fresh:
-            ctx.reset()  # (a context grown by _context carried counts over: reset drops them too)
+        # carry=False: a context too small for the grown dictionary is replaced, never linked, so
+        # a previous query's NPE or device error cannot surface here; a kept one is reset
+        old = linker._ctx
+        ctx = linker._context(key, carry=False)
+        if ctx is old:
+            ctx.reset()
         if window is not None:
             ctx.set_window(*window)
         ctx.put_selection(self._store)

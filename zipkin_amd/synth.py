@@ -166,3 +166,25 @@ def encode_json_v2(cols: Columns, names) -> np.ndarray:
     out = np.empty(n, np.uint8)
     L.zdl_synth_json_v2(cols.n_spans, *ptrs, out.ctypes.data)
     return out
+
+
+def put_trace_loop(ctx, cols: Columns, timestamps: bool = False) -> None:
+    """One zdl_put_trace per trace of `cols`, in order, from native code (libzdl_synth's
+    zdl_synth_put_trace_loop): the call pattern of the reference's putTrace callers
+    (InMemoryStorage.java:340, AggregateDependencies.java:81) as a JNI shim would drive it."""
+    from . import _native as N
+    L = _synth()
+    if not hasattr(L, "_ptl"):
+        L.zdl_synth_put_trace_loop.restype = C.c_int
+        L.zdl_synth_put_trace_loop.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(N.SpanCols), C.c_void_p,
+                                               C.c_uint64, C.POINTER(C.c_uint64)]
+        L._ptl = True
+    p = N._ptr
+    sc = N.SpanCols(p(cols.trace_lo), p(cols.id), p(cols.parent_id), p(cols.local_svc), p(cols.remote_svc),
+                    p(cols.local_ip4), p(cols.local_ip6), p(cols.port_flags),
+                    p(cols.timestamp) if timestamps else None)
+    at = C.c_uint64(0)
+    fn = C.cast(N.lib().zdl_put_trace, C.c_void_p)
+    rc = L.zdl_synth_put_trace_loop(fn, ctx.h, C.byref(sc), cols.offsets.ctypes.data, cols.n_traces, C.byref(at))
+    if rc != 0:
+        ctx.check(rc)
