@@ -403,3 +403,23 @@ def test_mid_size_messy_traces_vs_cpp(sparse, wave, monkeypatch):
     assert got == sorted(_oracle(cols))
     st, p, c, n, e = ref.link(cols, window=(base_ms + 60_000, 30_000), threads=16)
     assert st == 0 and len(p) > 100 and windowed == sorted(_tuples(p, c, n, e))
+
+
+@pytest.mark.parametrize("config", ["c2", "c4"])
+def test_comm_job_of_one_rank_insertion_order(config):
+    """An insertion-order context joined to a one-rank job: zdl_link(ZDL_ORDER_INSERTION) sums
+    the tables and MIN-reduces the rank-tagged first-seen ranks (comm_sum_ord, zdl_xplan.h);
+    with one rank that is the single context's exact list order, the C++ restatement's."""
+    w = synth.CONFIGS[config].scaled(50_000)
+    cols = synth.generate(w)
+    S = w.total_services
+    ctx = N.Context(S, insertion_order=True)
+    ctx.comm_init(N.Context.comm_unique_id(), 0, 1)
+    ctx.put_spans(cols)
+    got = list(_tuples(*ctx.link(N.ZDL_ORDER_INSERTION)))
+    ctx.put_spans(cols)
+    twice = list(_tuples(*ctx.link(N.ZDL_ORDER_INSERTION)))
+    ctx.close()
+    exp = list(_oracle(cols))
+    assert got == exp
+    assert twice == [(a, b, 2 * n, 2 * e) for a, b, n, e in exp]

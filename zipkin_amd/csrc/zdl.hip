@@ -32,6 +32,7 @@
 #include "../../include/zdl.h"
 #include "zdl_algo.h"
 #include "zdl_sparse.h"
+#include "zdl_xplan.h"
 
 namespace zdl {
 
@@ -1536,6 +1537,7 @@ struct zdl_ctx {
   ncclComm_t comm = nullptr;
   int comm_rank = 0, comm_world = 1;
   DevBuf<unsigned long long> red_call, red_err;  // the summed tables
+  DevBuf<unsigned long long> red_first;          // insertion order: the job's first ranks (MIN)
   // sparse combine (device groups / jobs above 1024 services): every device's or rank's sorted
   // list gathered here (cell, call, err), summed into gacc (sparse_add: DependencyLinker.merge)
   DevBuf<uint32_t> gx_cell;
@@ -1880,6 +1882,7 @@ void zdl_destroy(zdl_ctx* c) {
   stage_free(c);
   c->red_call.release();
   c->red_err.release();
+  c->red_first.release();
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (auto& r : c->rank) r.release();
@@ -3150,7 +3153,8 @@ static void sort_output(zdl_ctx* c, size_t n) {
 
 // zdl_link in ZDL_ORDER_INSERTION: the non-zero cells with their first-addLink ranks
 // (k_merge_compact over the context's tables), ordered by rank.
-static int link_insertion(zdl_ctx* c, zdl_links* out) {
+static int link_insertion(zdl_ctx* c, zdl_links* out, const unsigned long long* call,
+                          const unsigned long long* errc, const unsigned long long* first_rank) {
   const uint64_t SS = (uint64_t)c->rows * c->S;
   HIP_TRY(c, c->o_p.ensure(SS));
   HIP_TRY(c, c->o_c.ensure(SS));
@@ -3158,8 +3162,8 @@ static int link_insertion(zdl_ctx* c, zdl_links* out) {
   HIP_TRY(c, c->o_err.ensure(SS));
   HIP_TRY(c, c->o_first.ensure(SS));
   HIP_TRY(c, hipMemsetAsync(c->count.p, 0, 8, c->stream));
-  hipLaunchKernelGGL(k_merge_compact, dim3((unsigned)((SS + 255) / 256)), dim3(256), 0, c->stream, c->call.p,
-                     c->errc.p, c->first.p, SS, c->S, c->count.p, c->o_p.p, c->o_c.p, c->o_call.p, c->o_err.p,
+  hipLaunchKernelGGL(k_merge_compact, dim3((unsigned)((SS + 255) / 256)), dim3(256), 0, c->stream, call,
+                     errc, first_rank, SS, c->S, c->count.p, c->o_p.p, c->o_c.p, c->o_call.p, c->o_err.p,
                      c->o_first.p);
   HIP_TRY(c, hipGetLastError());
   unsigned long long m = 0;
@@ -3288,6 +3292,7 @@ static int link_sorted(zdl_ctx* c, const unsigned long long* call, const unsigne
 }
 
 static int comm_sum_tables(zdl_ctx* c);  // multi-process job: every rank's tables summed (below)
+static int comm_sum_ord(zdl_ctx* c);     // ... and, insertion order, the rank-tagged first ranks' MIN
 
 // Four byte ranges [off, off + len) copied from HBM to mapped pinned host memory (same offsets
 // on both sides; offsets multiples of 8, lengths multiples of 4), 8 bytes a lane, grid-stride.
@@ -3427,7 +3432,12 @@ int zdl_link(zdl_ctx* c, int order, zdl_links* out) {
   if (order == ZDL_ORDER_INSERTION) {
     if (!c->ord) return fail(c, ZDL_EINVAL, "ZDL_ORDER_INSERTION needs a ZDL_FLAG_INSERTION_ORDER context");
     HIP_TRY(c, enter(c));
-    return link_insertion(c, out);
+    if (c->comm) {  // a rank of a job: DependencyLinker.merge over the ranks' lists in rank order
+      const int rc = comm_sum_ord(c);
+      if (rc != ZDL_OK) return rc;
+      return link_insertion(c, out, c->red_call.p, c->red_err.p, c->red_first.p);
+    }
+    return link_insertion(c, out, c->call.p, c->errc.p, c->first.p);
   }
   if (order != ZDL_ORDER_SORTED) return fail(c, ZDL_EINVAL, "zdl_link: order must be ZDL_ORDER_SORTED or ZDL_ORDER_INSERTION");
   HIP_TRY(c, enter(c));
@@ -3940,39 +3950,39 @@ static int group_reduce(zdl_ctx* g, unsigned long long* rcall, unsigned long lon
 // an allgather of compacted (pair, call, err) instead of S x S tables.
 static int group_link_sparse(zdl_ctx* g, zdl_links* out) {
   zdl_ctx* s0 = g->sub[0];
-  const size_t N = g->sub.size();
-  std::vector<uint64_t> n(N), at(N + 1, 0);
-  for (size_t d = 0; d < N; ++d) {
-    n[d] = g->sub[d]->acc.n;
-    at[d + 1] = at[d] + n[d];
-  }
-  const uint64_t total = at[N];
+  const int N = (int)g->sub.size();
+  std::vector<uint64_t> n((size_t)N);
+  for (int d = 0; d < N; ++d) n[d] = g->sub[d]->acc.n;
+  const zdl_xplan::Plan plan = zdl_xplan::gather_plan(n.data(), N, false);  // every list to device 0
+  const uint64_t total = plan.total();
   HIP_TRY(g, enter(s0));
   HIP_TRY(g, s0->gx_cell.ensure(total));
   HIP_TRY(g, s0->gx_call.ensure(total));
   HIP_TRY(g, s0->gx_err.ensure(total));
   ncclResult_t r = ncclGroupStart();
-  for (size_t d = 1; d < N && r == ncclSuccess; ++d) {
-    zdl_ctx* s = g->sub[d];
-    if (!n[d]) continue;
+  for (const zdl_xplan::Xfer& x : plan.ops) {
+    if (x.src == x.dst || r != ncclSuccess) continue;  // device 0's own list: a copy below
+    zdl_ctx* s = g->sub[x.src];
+    zdl_ctx* t = g->sub[x.dst];
     (void)hipSetDevice(s->device);
-    r = ncclSend(s->acc.cell, n[d], ncclUint32, 0, g->comms[d], s->stream);
-    if (r == ncclSuccess) r = ncclSend(s->acc.call, n[d], ncclUint64, 0, g->comms[d], s->stream);
-    if (r == ncclSuccess) r = ncclSend(s->acc.err, n[d], ncclUint64, 0, g->comms[d], s->stream);
-    (void)hipSetDevice(s0->device);
-    if (r == ncclSuccess) r = ncclRecv(s0->gx_cell.p + at[d], n[d], ncclUint32, (int)d, g->comms[0], s0->stream);
-    if (r == ncclSuccess) r = ncclRecv(s0->gx_call.p + at[d], n[d], ncclUint64, (int)d, g->comms[0], s0->stream);
-    if (r == ncclSuccess) r = ncclRecv(s0->gx_err.p + at[d], n[d], ncclUint64, (int)d, g->comms[0], s0->stream);
+    r = ncclSend(s->acc.cell, x.n, ncclUint32, x.dst, g->comms[x.src], s->stream);
+    if (r == ncclSuccess) r = ncclSend(s->acc.call, x.n, ncclUint64, x.dst, g->comms[x.src], s->stream);
+    if (r == ncclSuccess) r = ncclSend(s->acc.err, x.n, ncclUint64, x.dst, g->comms[x.src], s->stream);
+    (void)hipSetDevice(t->device);
+    if (r == ncclSuccess) r = ncclRecv(t->gx_cell.p + x.at, x.n, ncclUint32, x.src, g->comms[x.dst], t->stream);
+    if (r == ncclSuccess) r = ncclRecv(t->gx_call.p + x.at, x.n, ncclUint64, x.src, g->comms[x.dst], t->stream);
+    if (r == ncclSuccess) r = ncclRecv(t->gx_err.p + x.at, x.n, ncclUint64, x.src, g->comms[x.dst], t->stream);
   }
   const ncclResult_t r2 = ncclGroupEnd();
   (void)hipSetDevice(s0->device);
   if (r != ncclSuccess || r2 != ncclSuccess)
     return fail(g, ZDL_EDEVICE, std::string("device group: ncclSend/Recv: ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
   hipStream_t st = s0->stream;
-  if (n[0]) {
-    HIP_TRY(g, hipMemcpyAsync(s0->gx_cell.p, s0->acc.cell, n[0] * 4, hipMemcpyDeviceToDevice, st));
-    HIP_TRY(g, hipMemcpyAsync(s0->gx_call.p, s0->acc.call, n[0] * 8, hipMemcpyDeviceToDevice, st));
-    HIP_TRY(g, hipMemcpyAsync(s0->gx_err.p, s0->acc.err, n[0] * 8, hipMemcpyDeviceToDevice, st));
+  for (const zdl_xplan::Xfer& x : plan.ops) {
+    if (x.src != x.dst) continue;
+    HIP_TRY(g, hipMemcpyAsync(s0->gx_cell.p + x.at, s0->acc.cell, x.n * 4, hipMemcpyDeviceToDevice, st));
+    HIP_TRY(g, hipMemcpyAsync(s0->gx_call.p + x.at, s0->acc.call, x.n * 8, hipMemcpyDeviceToDevice, st));
+    HIP_TRY(g, hipMemcpyAsync(s0->gx_err.p + x.at, s0->acc.err, x.n * 8, hipMemcpyDeviceToDevice, st));
   }
   s0->gacc.n = 0;
   int kb = 1;
@@ -4027,6 +4037,37 @@ static int comm_sum_tables(zdl_ctx* c) {
   return ZDL_OK;
 }
 
+// Each rank's first-seen ranks tagged with the job rank above them (zdl_xplan::ord_tag)
+__global__ void k_ord_tag(const unsigned long long* __restrict__ first, unsigned long long* __restrict__ out,
+                          uint64_t n, int rank) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    out[i] = zdl_xplan::ord_tag(first[i], rank);
+}
+
+// Insertion order across a job (zdl_xplan.h): the sums as comm_sum_tables, and one ncclMin of
+// the rank-tagged first ranks, so a pair sits where DependencyLinker.merge over the ranks'
+// link() lists, concatenated in rank order, first sees it (DependencyLinker.java:189-204).
+static int comm_sum_ord(zdl_ctx* c) {
+  if (c->span_base >= zdl_xplan::ORD_POS_LIMIT)
+    return fail(c, ZDL_EINVAL, "insertion order across ranks: more than 2^34 spans put on this rank");
+  const size_t SS = (size_t)c->rows * c->S;
+  HIP_TRY(c, c->red_call.ensure(SS));
+  HIP_TRY(c, c->red_err.ensure(SS));
+  HIP_TRY(c, c->red_first.ensure(SS));
+  hipLaunchKernelGGL(k_ord_tag, dim3((unsigned)std::min<size_t>((SS + 255) / 256, 4096)), dim3(256), 0, c->stream,
+                     c->first.p, c->red_first.p, (uint64_t)SS, c->comm_rank);
+  HIP_TRY(c, hipGetLastError());
+  ncclResult_t r = ncclGroupStart();
+  if (r == ncclSuccess) r = ncclAllReduce(c->call.p, c->red_call.p, SS, ncclUint64, ncclSum, c->comm, c->stream);
+  if (r == ncclSuccess) r = ncclAllReduce(c->errc.p, c->red_err.p, SS, ncclUint64, ncclSum, c->comm, c->stream);
+  if (r == ncclSuccess)
+    r = ncclAllReduce(c->red_first.p, c->red_first.p, SS, ncclUint64, ncclMin, c->comm, c->stream);
+  const ncclResult_t r2 = ncclGroupEnd();
+  if (r != ncclSuccess || r2 != ncclSuccess)
+    return fail(c, ZDL_EDEVICE, std::string("ncclAllReduce: ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
+  return ZDL_OK;
+}
+
 // Multi-process jobs above 1024 services: the ranks' list lengths by ncclAllGather, then every
 // rank's list to every rank (ncclSend / ncclRecv, exact lengths: an all-gather of unequal
 // parts), summed per cell on each rank (sparse_add) - every rank returns the job's links.
@@ -4037,35 +4078,35 @@ static int comm_sum_sparse(zdl_ctx* c) {
   HIP_TRY(c, hipMemcpyAsync(c->gx_n.p + W, &c->acc.n, 8, hipMemcpyHostToDevice, st));
   ncclResult_t r = ncclAllGather(c->gx_n.p + W, c->gx_n.p, 1, ncclUint64, c->comm, st);
   if (r != ncclSuccess) return fail(c, ZDL_EDEVICE, std::string("ncclAllGather: ") + ncclGetErrorString(r));
-  std::vector<uint64_t> n(W), at(W + 1, 0);
+  std::vector<uint64_t> n((size_t)W);
   HIP_TRY(c, hipMemcpyAsync(n.data(), c->gx_n.p, 8 * (size_t)W, hipMemcpyDeviceToHost, st));
   HIP_TRY(c, hipStreamSynchronize(st));
-  for (int k = 0; k < W; ++k) at[k + 1] = at[k] + n[k];
-  const uint64_t total = at[W];
+  const zdl_xplan::Plan plan = zdl_xplan::gather_plan(n.data(), W, true);  // every list to every rank
+  const uint64_t total = plan.total();
   HIP_TRY(c, c->gx_cell.ensure(total));
   HIP_TRY(c, c->gx_call.ensure(total));
   HIP_TRY(c, c->gx_err.ensure(total));
   r = ncclGroupStart();
-  for (int k = 0; k < W && r == ncclSuccess; ++k) {
-    if (k == me) continue;
-    if (n[me]) {
-      r = ncclSend(c->acc.cell, n[me], ncclUint32, k, c->comm, st);
-      if (r == ncclSuccess) r = ncclSend(c->acc.call, n[me], ncclUint64, k, c->comm, st);
-      if (r == ncclSuccess) r = ncclSend(c->acc.err, n[me], ncclUint64, k, c->comm, st);
-    }
-    if (r == ncclSuccess && n[k]) {
-      r = ncclRecv(c->gx_cell.p + at[k], n[k], ncclUint32, k, c->comm, st);
-      if (r == ncclSuccess) r = ncclRecv(c->gx_call.p + at[k], n[k], ncclUint64, k, c->comm, st);
-      if (r == ncclSuccess) r = ncclRecv(c->gx_err.p + at[k], n[k], ncclUint64, k, c->comm, st);
+  for (const zdl_xplan::Xfer& x : plan.ops) {
+    if (x.src == x.dst || r != ncclSuccess) continue;
+    if (x.src == me) {
+      r = ncclSend(c->acc.cell, x.n, ncclUint32, x.dst, c->comm, st);
+      if (r == ncclSuccess) r = ncclSend(c->acc.call, x.n, ncclUint64, x.dst, c->comm, st);
+      if (r == ncclSuccess) r = ncclSend(c->acc.err, x.n, ncclUint64, x.dst, c->comm, st);
+    } else if (x.dst == me) {
+      r = ncclRecv(c->gx_cell.p + x.at, x.n, ncclUint32, x.src, c->comm, st);
+      if (r == ncclSuccess) r = ncclRecv(c->gx_call.p + x.at, x.n, ncclUint64, x.src, c->comm, st);
+      if (r == ncclSuccess) r = ncclRecv(c->gx_err.p + x.at, x.n, ncclUint64, x.src, c->comm, st);
     }
   }
   const ncclResult_t r2 = ncclGroupEnd();
   if (r != ncclSuccess || r2 != ncclSuccess)
     return fail(c, ZDL_EDEVICE, std::string("ncclSend/Recv: ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
-  if (n[me]) {
-    HIP_TRY(c, hipMemcpyAsync(c->gx_cell.p + at[me], c->acc.cell, n[me] * 4, hipMemcpyDeviceToDevice, st));
-    HIP_TRY(c, hipMemcpyAsync(c->gx_call.p + at[me], c->acc.call, n[me] * 8, hipMemcpyDeviceToDevice, st));
-    HIP_TRY(c, hipMemcpyAsync(c->gx_err.p + at[me], c->acc.err, n[me] * 8, hipMemcpyDeviceToDevice, st));
+  for (const zdl_xplan::Xfer& x : plan.ops) {
+    if (x.src != me || x.dst != me) continue;
+    HIP_TRY(c, hipMemcpyAsync(c->gx_cell.p + x.at, c->acc.cell, x.n * 4, hipMemcpyDeviceToDevice, st));
+    HIP_TRY(c, hipMemcpyAsync(c->gx_call.p + x.at, c->acc.call, x.n * 8, hipMemcpyDeviceToDevice, st));
+    HIP_TRY(c, hipMemcpyAsync(c->gx_err.p + x.at, c->acc.err, x.n * 8, hipMemcpyDeviceToDevice, st));
   }
   c->gacc.n = 0;
   int kb = 1;
@@ -4089,7 +4130,9 @@ int zdl_comm_init(zdl_ctx* c, const uint8_t* id, int rank, int world) {
   if (c->link_pending >= 0) return fail(c, ZDL_EINVAL, "zdl_comm_init: a started link is not finished (zdl_link_finish)");
   if (const int frc = stage_flush(c)) return frc;  // staged putTrace calls come first
   if (!c->sub.empty()) return fail(c, ZDL_EINVAL, "zdl_comm_init: a device group has its own communicator");
-  if (c->ord || c->days) return fail(c, ZDL_EINVAL, "zdl_comm_init: insertion order and daily buckets are per process");
+  if (c->days) return fail(c, ZDL_EINVAL, "zdl_comm_init: daily buckets are per process");
+  if (c->ord && world > zdl_xplan::ORD_MAX_WORLD)
+    return fail(c, ZDL_EINVAL, "zdl_comm_init: insertion order across at most 64 ranks");
   if (c->comm) return fail(c, ZDL_EINVAL, "zdl_comm_init: already joined");
   HIP_TRY(c, enter(c));
   ncclUniqueId u;
