@@ -175,12 +175,14 @@ struct Args {
   const uint32_t* grest;    // and then the back-list indexes k_tail links instead of the whole back
   const uint32_t* grest_n;  // list (the giant ones dropped; the ones the tier rejected appended)
   uint8_t* bstat;           // k_big's verdict per back-list index (1 linked, 2 exact path), or null
+  uint32_t* exact;          // with bstat: the back-list indexes k_big left to k_tail's exact path,
+  uint32_t* exact_n;        // appended as found (k_tail walks this list, not the whole back list)
   uint32_t* tick_big;       // k_big's trace tickets
   uint32_t kb_small;        // k_big<256> takes the traces of at most this many spans (<= KB_SMALL)
 };
 // The counter block of one put (two alternate by put, so no put issues a memset)
 enum : int { CTR_MID = 0, CTR_CX = 1, CTR_LARGE = 2, CTR_TICK_LARGE = 3, CTR_TICK_MID = 4, CTR_RETRY = 5,
-             CTR_TICK_BIG = 6, CTR_N = 8 };  // (CTR_TICK_BIG + 1: k_big<256>'s tickets)
+             CTR_TICK_BIG = 6, CTR_EXACT = 8, CTR_N = 10 };  // (CTR_TICK_BIG + 1: k_big<256>'s tickets)
 constexpr int CTR_DONE = 2 * CTR_N;  // k_tail's finished-workgroup count (after both blocks)
 
 #include "zdl_full.inc"  // the full per-window emulation (k_tail's first part)
@@ -1286,7 +1288,9 @@ __global__ void __launch_bounds__(TAIL_WG, 1) k_tail(Args A) {
   // simple), one workgroup each, by ticket (the next one fetched while this trace is linked),
   // so that a giant trace delays only its own workgroup
   __shared__ uint32_t sh_j;
-  const uint32_t nlarge = A.grest ? *A.grest_n : *A.large_count;
+  // when k_big ran, only the back-list traces it left for the exact path (its compacted list;
+  // walking the whole back list by ticket cost a returning atomic per entry: ~0.3 ms at C5)
+  const uint32_t nlarge = A.bstat ? *A.exact_n : A.grest ? *A.grest_n : *A.large_count;
   const uint32_t nbig = nlarge + (A.wb_max ? *A.retry_count : 0u);
   if (nbig) {
     if (threadIdx.x == 0) sh_j = atomicAdd(A.tick_large, 1u);
@@ -1297,9 +1301,10 @@ __global__ void __launch_bounds__(TAIL_WG, 1) k_tail(Args A) {
       if (j >= nbig) break;
       if (threadIdx.x == 0) sh_j = atomicAdd(A.tick_large, 1u);
       const bool back = j < nlarge;
-      const uint32_t bi = back ? (A.grest ? A.grest[j] : A.big_cap - 1u - j) : A.retry[j - nlarge];
-      // k_big's verdict (or the giant tier's when k_big did not run): 1 linked, 2 the exact path
-      const uint8_t gs = !back ? 0 : A.bstat ? A.bstat[bi] : A.gstat ? A.gstat[bi] : 0;  // (uniform)
+      const uint32_t bi = !back ? A.retry[j - nlarge]
+                                : A.bstat ? A.exact[j] : A.grest ? A.grest[j] : A.big_cap - 1u - j;
+      // the giant tier's verdict when k_big did not run: 1 linked, 2 the exact path
+      const uint8_t gs = !back ? 0 : A.bstat ? 2 : A.gstat ? A.gstat[bi] : 0;  // (uniform)
       if (gs != 1) big_one<ORD>(A, lds, tail_block_bytes(WINDOW), bi, back && gs == 0);
     }
   }
@@ -1363,7 +1368,10 @@ __global__ void __launch_bounds__(NT, NT == 256 ? 4 : 1) k_big(Args A) {
       const uint8_t gs = A.gstat ? A.gstat[bi] : 0;  // the giant tier's verdict (uniform)
       uint8_t st = gs;
       if (gs == 0) st = big_one<0, true, NT>(A, lds, lds_bytes, bi, true) ? 1 : 2;
-      if (threadIdx.x == 0) A.bstat[bi] = st;
+      if (threadIdx.x == 0) {
+        A.bstat[bi] = st;
+        if (st == 2) A.exact[atomicAdd(A.exact_n, 1u)] = bi;  // rare: not simple, or the tier rejected it
+      }
     }
   }
 }
@@ -1508,6 +1516,7 @@ struct zdl_ctx {
   DevBuf<uint32_t> o_fa, o_fb, o_bfs;
   // per-put scratch
   DevBuf<uint32_t> big_list, counters;
+  DevBuf<uint32_t> big_exact_list;  // k_big -> k_tail: the back-list traces for the exact path
   DevBuf<uint8_t> big_stat;  // k_big's verdicts  // counters: two CTR_N blocks alternating by put, then done
   DevBuf<uint32_t> retry;  // k_tail: wave_big traces for the exact path
   uint32_t epoch = 0;
@@ -1888,7 +1897,7 @@ void zdl_destroy(zdl_ctx* c) {
   for (auto& r : c->rank) r.release();
   c->call.release(); c->errc.release(); c->status.release();
   c->first.release(); c->day_first.release(); c->o_key.release(); c->o_fa.release(); c->o_fb.release(); c->o_bfs.release();
-  c->big_list.release(); c->big_stat.release(); c->counters.release(); c->retry.release();
+  c->big_list.release(); c->big_stat.release(); c->big_exact_list.release(); c->counters.release(); c->retry.release();
   c->cx_win.release();
   if (c->prof_on && c->prof.p) {
     unsigned long long h[12] = {};
@@ -2104,14 +2113,31 @@ __global__ void k_seg_build(const uint64_t* __restrict__ lg_start, const uint32_
   }
 }
 
-__global__ void k_seg_copy(const uint32_t* __restrict__ lg, const uint64_t* __restrict__ src,
-                           const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ at, uint64_t nseg,
-                           uint32_t* __restrict__ lin) {
-  for (uint64_t sgm = blockIdx.x; sgm < nseg; sgm += gridDim.x) {
-    const uint32_t n = cnt[sgm];
-    const uint32_t* in = lg + src[sgm];
-    uint32_t* out = lin + at[sgm];
-    for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) out[j] = in[j];
+// The segments gathered into one array, by output tiles of SEG_TILE entries (one workgroup
+// each: the first segment found by a binary search of the offsets, then walked): a segment
+// per workgroup left a 400 k-entry giant trace to one workgroup (243 us at C5).
+constexpr uint32_t SEG_TILE = 4096;
+__global__ void __launch_bounds__(256) k_seg_copy(const uint32_t* __restrict__ lg, const uint64_t* __restrict__ src,
+                                                  const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ at,
+                                                  uint64_t nseg, uint64_t E, uint32_t* __restrict__ lin) {
+  __shared__ uint64_t sh_s;
+  const uint64_t t0 = (uint64_t)blockIdx.x * SEG_TILE, t1 = t0 + SEG_TILE < E ? t0 + SEG_TILE : E;
+  if (threadIdx.x == 0) {  // the last segment starting at or before t0
+    uint64_t lo = 0, hi = nseg;
+    while (hi - lo > 1) {
+      const uint64_t mid = (lo + hi) / 2;
+      if (at[mid] <= t0) lo = mid;
+      else hi = mid;
+    }
+    sh_s = lo;
+  }
+  __syncthreads();
+  for (uint64_t sg = sh_s; sg < nseg; ++sg) {
+    const uint64_t a = at[sg];
+    if (a >= t1) break;
+    const uint64_t b0 = a > t0 ? a : t0, e = a + cnt[sg], b1 = e < t1 ? e : t1;
+    const uint32_t* in = lg + src[sg];
+    for (uint64_t j = b0 + threadIdx.x; j < b1; j += 256) lin[j] = in[j - a];
   }
 }
 
@@ -2144,8 +2170,8 @@ static int sparse_finish(zdl_ctx* c, uint32_t ep, uint32_t lW, uint64_t n_spans,
   if (E > 4 * n_spans) return fail(c, ZDL_EDEVICE, "sparse: more links than the log holds");
   if (E == 0) return ZDL_OK;
   HIP_TRY(c, c->lin.ensure(E));
-  hipLaunchKernelGGL(k_seg_copy, dim3((unsigned)std::min<uint64_t>(nseg, 65536)), dim3(256), 0, s, c->lg.p,
-                     c->seg_src.p, c->seg_n.p, c->seg_off.p, nseg, c->lin.p);
+  hipLaunchKernelGGL(k_seg_copy, dim3((unsigned)((E + SEG_TILE - 1) / SEG_TILE)), dim3(256), 0, s, c->lg.p,
+                     c->seg_src.p, c->seg_n.p, c->seg_off.p, nseg, E, c->lin.p);
   HIP_TRY(c, hipGetLastError());
   int kb = 1;
   while ((1ull << kb) < (uint64_t)c->S * c->S) ++kb;
@@ -2335,6 +2361,7 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   const int grid = c->grid, lgrid = c->cus * lk::wgs_per_cu;  // k_link: two 16-wave workgroups per CU
   HIP_TRY(c, c->big_list.ensure(n_traces));
   HIP_TRY(c, c->big_stat.ensure(n_traces));
+  HIP_TRY(c, c->big_exact_list.ensure(n_traces));
   // queued windows: at most one per trace; mode 3 (insertion order) uses one slot per trace
   HIP_TRY(c, c->cx_win.ensure(2 * ((c->ord || c->days) ? n_traces : std::min<uint64_t>(n_traces, n_spans))));
   Args A{};
@@ -2360,6 +2387,7 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   A.err = c->errc.p;
   A.big_list = c->big_list.p;
   A.bstat = c->ord ? nullptr : c->big_stat.p;  // k_big runs (insertion order: every big trace exact)
+  A.exact = c->big_exact_list.p;
   const uint32_t ep = c->epoch & 1u;
   uint32_t* ctr = c->counters.p + ep * CTR_N;
   A.big_count = ctr + CTR_MID;
@@ -2368,6 +2396,7 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   A.tick_mid = ctr + CTR_TICK_MID;
   A.retry_count = ctr + CTR_RETRY;
   A.tick_big = ctr + CTR_TICK_BIG;
+  A.exact_n = ctr + CTR_EXACT;
   {
     static const uint32_t kbs = [] {
       const char* e = getenv("ZDL_KB_SMALL");  // A/B and tests: 0 = every trace in k_big<1024>
