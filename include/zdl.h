@@ -194,8 +194,10 @@ int zdl_set_window(zdl_ctx* ctx, int64_t end_ts_ms, int64_t lookback_ms);
 
 /* putTrace over n_traces CSR-grouped traces from HOST buffers: trace t is spans
  * [trace_offsets[t], trace_offsets[t+1]) in storage order; trace_offsets has n_traces+1
- * entries, starts at 0 and ends at n_spans. Synchronous. Counts accumulate in the
- * context across calls. On ZDL_EREF_NPE the counts are unspecified until zdl_reset.
+ * entries, starts at 0 and ends at n_spans (at most 2^32 - 129 spans a put: split larger
+ * inputs, the counts accumulate). Synchronous. Counts accumulate in the context across
+ * calls. On ZDL_EREF_NPE the traces whose Trace.merge throws add nothing; the others of the
+ * batch are counted (the status stays NPE until zdl_reset; zdl_put_trace clears it).
  * trace_offsets == NULL: the spans are ungrouped; they are grouped on the device by
  * trace_lo (stable in `ord`, else input order; n_traces is ignored, n_spans < 2^32),
  * as InMemoryStorage.getDependencies groups by lowTraceId (InMemoryStorage.java:323-332,

@@ -14,6 +14,8 @@
 // zdl_link reads that (or compacts the non-zero cells itself: k_compact_ordered /
 // k_compact) and sorts by service rank when ranks are set.
 #include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 #include <rccl/rccl.h>
 
 #include "zdl_group.h"
@@ -1565,12 +1567,14 @@ struct zdl_ctx {
   // the device-wide big-trace tier (zdl_giant.inc, sparse contexts): per-put lists and scratch
   int giant_min = 2048;  // traces longer than this (ZDL_GIANT_MIN; 0: off, k_tail's workgroups)
   DevBuf<uint32_t> gg_bi, gg_n, gg_tile0, gg_bad, gg_tile_g, gg_bstart, gg_blen, gg_meta, gg_H, gg_rest;
-  DevBuf<unsigned long long> gg_sc0, gg_sc1;
   DevBuf<unsigned char> gg_tmp;
   DevBuf<uint64_t> gg_base, gg_h0;
   DevBuf<unsigned long long> gg_root, gg_tsroot, gg_tsmin;
   DevBuf<int32_t> gg_rootidx;
   DevBuf<uint8_t> gg_stat;
+  GArgs gg_args{};            // the tier's arguments, from giant_prep to giant_run
+  hipEvent_t gg_ev = nullptr;  // k_g_prep's totals copied to h_gmeta
+  uint64_t gg_ntmax = 0;
   uint32_t* h_gmeta = nullptr;  // pinned: the tier's GM_* words
   int big_exact = 0;
   bool wave_big = true;  // ZDL_WAVE_BIG=0: every big trace takes a workgroup (tests compare both)  // ZDL_BIG_EXACT=1: big traces skip big_simple (tests compare both paths)
@@ -1609,6 +1613,11 @@ struct zdl_ctx {
   // kernel storing over PCIe held its CUs for the whole transfer (1.9 ms at C5), so the other
   // step in flight could not run beside it
   DevBuf<unsigned char> rec_dev;
+  // ZDL_REC_SDMA=1: the staged records go to the host on an SDMA engine (hsa_amd_memory_async_copy
+  // from a helper thread once the compaction's event fired) instead of k_pcie_copy's workgroups
+  std::thread rec_th;
+  int rec_th_rc = 0;
+  hipEvent_t rec_ev = nullptr;
   DevBuf<uint64_t> o_first;
   DevBuf<int32_t> mi_p, mi_c;
   DevBuf<int64_t> mi_call, mi_err;
@@ -1734,6 +1743,7 @@ static int resolve_lazy(zdl_ctx* c, bool wait);  // a lazy put's k_mid / k_tail 
 static int stage_flush(zdl_ctx* c);                // zdl_put_trace's staged traces as one put
 static void stage_drop(zdl_ctx* c);                // ... discarded (zdl_reset)
 static void stage_free(zdl_ctx* c);
+static int rec_wait(zdl_ctx* c);  // the SDMA record copy of the last link (ZDL_REC_SDMA)
 
 // splitmix64 finaliser (shard.py's): trace t goes to device splitmix64(trace_lo) % n
 inline uint64_t splitmix64(uint64_t x) {
@@ -1889,6 +1899,8 @@ void zdl_destroy(zdl_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)resolve_lazy(c, false);
   stage_free(c);
+  (void)rec_wait(c);
+  if (c->rec_ev) (void)hipEventDestroy(c->rec_ev);
   c->red_call.release();
   c->red_err.release();
   c->red_first.release();
@@ -1946,7 +1958,8 @@ void zdl_destroy(zdl_ctx* c) {
   for (auto* b : {&c->gg_bi, &c->gg_n, &c->gg_tile0, &c->gg_bad, &c->gg_tile_g, &c->gg_bstart, &c->gg_blen,
                   &c->gg_meta, &c->gg_H, &c->gg_rest})
     b->release();
-  c->gg_sc0.release(); c->gg_sc1.release(); c->gg_tmp.release();
+  c->gg_tmp.release();
+  if (c->gg_ev) (void)hipEventDestroy(c->gg_ev);
   c->gg_base.release(); c->gg_h0.release(); c->gg_root.release(); c->gg_tsroot.release(); c->gg_tsmin.release();
   c->gg_rootidx.release(); c->gg_stat.release();
   if (c->h_gmeta) (void)hipHostFree(c->h_gmeta);
@@ -2179,22 +2192,22 @@ static int sparse_finish(zdl_ctx* c, uint32_t ep, uint32_t lW, uint64_t n_spans,
   return ZDL_OK;
 }
 
-// The device-wide big-trace tier (zdl_giant.inc) between k_mid and k_tail, sparse contexts only:
-// their put is synchronous anyway (sparse_finish reads its counts), so reading how many traces
-// k_link listed for workgroups, and then the tier's sizes, costs no extra overlap. Sets A.gstat
-// when it ran; k_tail then skips the traces it linked.
-static int giant_run(zdl_ctx* c, Args& A, uint64_t n_spans, uint64_t n_traces) {
+// The device-wide big-trace tier (zdl_giant.inc), sparse contexts only. giant_prep runs right
+// after k_link, before k_mid: k_g_prep splits k_link's back list on the device's own count of it
+// and its totals are copied to pinned memory behind an event; giant_run (after k_mid's launch)
+// waits for that event only - k_mid keeps running meanwhile - and launches the tier's kernels,
+// which queue behind k_mid. Arrays indexed by back-list entry are sized by the bound on the
+// back list (every entry is longer than the wave tier's limit). Sets A.gstat / A.grest when the
+// tier has giant traces; k_big / k_tail then skip the traces it linked.
+static uint64_t giant_nl_bound(const Args& A, uint64_t n_spans, uint64_t n_traces) {
+  const uint64_t lim = std::max<uint64_t>(A.wb_max, (uint64_t)WSMALL) + 1;  // back-list traces are longer
+  return std::min<uint64_t>(n_traces, n_spans / lim + 1);
+}
+static int giant_prep(zdl_ctx* c, Args& A, uint64_t n_spans, uint64_t n_traces) {
   const hipStream_t s = c->stream;
   if (!c->h_gmeta) HIP_TRY(c, hipHostMalloc((void**)&c->h_gmeta, GM_WORDS * 4, hipHostMallocDefault));
-  HIP_TRY(c, hipMemcpyAsync(c->h_gmeta, A.large_count, 4, hipMemcpyDeviceToHost, s));
-  HIP_TRY(c, hipStreamSynchronize(s));
-  const uint32_t nl = c->h_gmeta[0];
-  if (nl == 0) return ZDL_OK;
-  if (nl > n_traces) return fail(c, ZDL_EDEVICE, "giant tier: inconsistent big-trace count");
-  // k_g_mark packs the giant and rest counts in 20 bits each of one scan word: a back list of
-  // 2^20 traces or more would carry into the next field, so the tier stands aside and k_tail
-  // takes the whole back list (A.grest stays null)
-  if (nl >= GMARK_MAX) return ZDL_OK;
+  if (!c->gg_ev) HIP_TRY(c, hipEventCreateWithFlags(&c->gg_ev, hipEventDisableTiming));
+  const uint64_t nl = giant_nl_bound(A, n_spans, n_traces);
   const uint64_t ntmax = n_spans / GT + nl + 1;
   HIP_TRY(c, c->gg_bi.ensure(nl));
   HIP_TRY(c, c->gg_n.ensure(nl));
@@ -2212,9 +2225,8 @@ static int giant_run(zdl_ctx* c, Args& A, uint64_t n_spans, uint64_t n_traces) {
   HIP_TRY(c, c->gg_blen.ensure(ntmax));
   HIP_TRY(c, c->gg_meta.ensure(GM_WORDS));
   HIP_TRY(c, c->gg_rest.ensure(nl));
-  HIP_TRY(c, c->gg_sc0.ensure(nl));
-  HIP_TRY(c, c->gg_sc1.ensure(nl));
-  GArgs G{};
+  GArgs& G = c->gg_args;
+  G = GArgs{};
   G.bi = c->gg_bi.p;
   G.base = c->gg_base.p;
   G.n = c->gg_n.p;
@@ -2232,31 +2244,27 @@ static int giant_run(zdl_ctx* c, Args& A, uint64_t n_spans, uint64_t n_traces) {
   G.gstat = c->gg_stat.p;
   G.gmin = (uint32_t)c->giant_min;
   G.rest = c->gg_rest.p;
-  G.sc0 = c->gg_sc0.p;
-  G.sc1 = c->gg_sc1.p;
-  G.nl = nl;
-  // the giant traces of the back list placed by two scans (tiles | counts, matrix sizes)
+  G.nl = (uint32_t)nl;
   HIP_TRY(c, hipMemsetAsync(c->gg_meta.p, 0, GM_WORDS * 4, s));
-  hipLaunchKernelGGL(k_g_mark, dim3((nl + 255) / 256), dim3(256), 0, s, A, G);
-  HIP_TRY(c, hipGetLastError());
-  size_t need = 0, need1 = 0;
-  HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(nullptr, need, c->gg_sc0.p, c->gg_sc0.p, (int)nl, s));
-  HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(nullptr, need1, c->gg_sc1.p, c->gg_sc1.p, (int)nl, s));
-  HIP_TRY(c, c->gg_tmp.ensure(std::max(need, need1)));
-  need = c->gg_tmp.n;
-  HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(c->gg_tmp.p, need, c->gg_sc0.p, c->gg_sc0.p, (int)nl, s));
-  need = c->gg_tmp.n;
-  HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(c->gg_tmp.p, need, c->gg_sc1.p, c->gg_sc1.p, (int)nl, s));
-  hipLaunchKernelGGL(k_g_write, dim3((nl + 255) / 256), dim3(256), 0, s, A, G);
+  hipLaunchKernelGGL(k_g_prep, dim3(1), dim3(GT), 0, s, A, G);
   HIP_TRY(c, hipGetLastError());
   HIP_TRY(c, hipMemcpyAsync(c->h_gmeta, c->gg_meta.p, GM_WORDS * 4, hipMemcpyDeviceToHost, s));
-  HIP_TRY(c, hipStreamSynchronize(s));
+  HIP_TRY(c, hipEventRecord(c->gg_ev, s));
+  c->gg_ntmax = ntmax;
+  return ZDL_OK;
+}
+
+static int giant_run(zdl_ctx* c, Args& A) {
+  const hipStream_t s = c->stream;
+  HIP_TRY(c, hipEventSynchronize(c->gg_ev));  // k_link and k_g_prep (k_mid may still run)
+  GArgs& G = c->gg_args;
   const uint32_t ng = c->h_gmeta[GM_G], nt = c->h_gmeta[GM_NT], maxn = c->h_gmeta[GM_MAXN], nh = c->h_gmeta[GM_NH];
   if (ng == 0) return ZDL_OK;  // k_tail takes the whole back list as usual
   A.gstat = c->gg_stat.p;  // every back-list entry has its verdict now
   A.grest = c->gg_rest.p;  // k_tail links the rest list only (k_g_par appends rejected giants)
   A.grest_n = c->gg_meta.p + GM_REST;
-  if (nt > ntmax || maxn > (uint32_t)GMAXN) return fail(c, ZDL_EDEVICE, "giant tier: inconsistent sizes");
+  if (nt > c->gg_ntmax || maxn > (uint32_t)GMAXN || nh == 0xFFFFFFFFu)
+    return fail(c, ZDL_EDEVICE, "giant tier: inconsistent sizes");
   HIP_TRY(c, c->gg_H.ensure(nh));
   G.H = c->gg_H.p;
   G.nt = nt;
@@ -2566,6 +2574,14 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
     c->times.grid = (uint32_t)grid;
     return ZDL_OK;
   }
+  const bool giant = c->sparse && c->giant_min > 0 && !c->ord && !c->days;
+  if (giant) {  // the giant tier's split of the back list, before k_mid (giant_prep)
+    const int grc = giant_prep(c, A, n_spans, n_traces);
+    if (grc != ZDL_OK) {
+      c->poisoned = true;  // k_link ran: the counter slots hold this put's counts
+      return grc;
+    }
+  }
   if (A.wb_max) {  // big_list's front (WSMALL < n <= WB_MAX spans): one wave per trace
     hipLaunchKernelGGL(k_mid, dim3((unsigned)c->cus * 4), dim3(MID_WG), 4 * WB_CARVE, c->stream, A);
     const hipError_t me = hipGetLastError();
@@ -2575,8 +2591,8 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
     }
   }
   ev_record(c, 3);
-  if (c->sparse && c->giant_min > 0 && !c->ord && !c->days) {  // the device-wide big-trace tier
-    const int grc = giant_run(c, A, n_spans, n_traces);
+  if (giant) {  // the device-wide big-trace tier (its prep ran before k_mid)
+    const int grc = giant_run(c, A);
     if (grc != ZDL_OK) {
       c->poisoned = true;  // k_link ran: the counter slots hold this put's counts
       return grc;
@@ -3045,7 +3061,9 @@ int zdl_put_spans_device(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans,
     return fail(c, ZDL_EINVAL, "missing column");
   if ((c->window || c->days) && !col->timestamp)
     return fail(c, ZDL_EINVAL, "window or days set but no timestamp column");
-  if (n_traces >= 0xffffffffull || n_spans >= (1ull << 40)) return fail(c, ZDL_EINVAL, "input too large");
+  // k_link plans its windows in 32-bit positions: a put holds at most 2^32 - 129 spans (split a
+  // larger input into several puts; the counts accumulate)
+  if (n_traces >= 0xffffffffull || n_spans > (1ull << 32) - 129) return fail(c, ZDL_EINVAL, "input too large");
   HIP_TRY(c, enter(c));
   if (!off) return put_spans_ungrouped(c, col, n_spans);
   return put_spans_link(c, col, n_spans, off, n_traces);
@@ -3299,6 +3317,7 @@ static int link_sorted(zdl_ctx* c, const unsigned long long* call, const unsigne
     if (drc != ZDL_OK) return drc;
     HIP_TRY(c, hipMemcpyAsync(c->h_meta, c->status.p, 16, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (const int wrc = rec_wait(c)) return wrc;
     put_times(c);
     c->times.compact_ms = ev_ms(c, 5, 6);
     const int rc = status_code(c, (uint32_t)c->h_meta[0]);
@@ -3355,6 +3374,7 @@ static bool rec_dma() {
 }
 
 static int ensure_rec(zdl_ctx* c, uint64_t m) {
+  if (const int wrc = rec_wait(c)) return wrc;
   if (m <= c->h_rec_cap) return ZDL_OK;
   c->rec_dev.release();
   if (c->h_rec) (void)hipHostFree(c->h_rec);
@@ -3377,9 +3397,71 @@ static int ensure_rec(zdl_ctx* c, uint64_t m) {
 // (k_pcie_copy: PCIe-bound at any width, so it leaves the other CUs to the next put's kernels;
 // hipMemcpyAsync ran rocclr's copyBuffer blit kernels across the whole GPU and slowed the
 // concurrent k_link from 0.66 to 2.1 ms, profiles/r03g_c5_timeline.txt).
+static bool rec_sdma() {  // default on; ZDL_REC_SDMA=0 (A/B): k_pcie_copy's workgroups instead
+  static const bool on = [] {
+    const char* e = getenv("ZDL_REC_SDMA");
+    return !(e && e[0] == '0');
+  }();
+  return on && !rec_dma();
+}
+
+// The four record columns [off, off + len) from HBM to the pinned host columns by SDMA copies
+// (ROCr's hsa_amd_memory_async_copy: a copy engine, no workgroups), waited for here.
+static int sdma_copy(unsigned char* dst, const unsigned char* src, const size_t* off, const size_t* len) {
+  hsa_amd_pointer_info_t ps{}, pd{};
+  ps.size = sizeof ps;
+  pd.size = sizeof pd;
+  if (hsa_amd_pointer_info(src, &ps, nullptr, nullptr, nullptr) != HSA_STATUS_SUCCESS ||
+      hsa_amd_pointer_info(dst, &pd, nullptr, nullptr, nullptr) != HSA_STATUS_SUCCESS)
+    return ZDL_EDEVICE;
+  hsa_signal_t sig;
+  if (hsa_signal_create(4, 0, nullptr, &sig) != HSA_STATUS_SUCCESS) return ZDL_EDEVICE;
+  int rc = ZDL_OK;
+  int issued = 0;
+  for (int k = 0; k < 4; ++k) {
+    if (len[k] == 0) {
+      hsa_signal_subtract_screlease(sig, 1);
+      continue;
+    }
+    if (hsa_amd_memory_async_copy(dst + off[k], pd.agentOwner, src + off[k], ps.agentOwner, len[k], 0, nullptr, sig) !=
+        HSA_STATUS_SUCCESS) {
+      rc = ZDL_EDEVICE;
+      hsa_signal_subtract_screlease(sig, 4 - k);  // the copies not issued
+      break;
+    }
+    ++issued;
+  }
+  (void)issued;
+  while (hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED) >= 1) {
+  }
+  hsa_signal_destroy(sig);
+  return rc;
+}
+
+static int rec_wait(zdl_ctx* c) {
+  if (!c->rec_th.joinable()) return ZDL_OK;
+  c->rec_th.join();
+  const int rc = c->rec_th_rc;
+  c->rec_th_rc = ZDL_OK;
+  return rc == ZDL_OK ? ZDL_OK : fail(c, rc, "SDMA copy of the link records failed");
+}
+
 static int rec_download(zdl_ctx* c, uint64_t m) {
   const size_t cap = c->h_rec_cap;
   if (m == 0) return ZDL_OK;
+  if (rec_sdma()) {  // ZDL_REC_SDMA=1: a helper thread waits for the compaction, then SDMA
+    if (!c->rec_ev) HIP_TRY(c, hipEventCreateWithFlags(&c->rec_ev, hipEventDisableTiming));
+    HIP_TRY(c, hipEventRecord(c->rec_ev, c->stream));
+    if (const int wrc = rec_wait(c)) return wrc;
+    const size_t off[4] = {0, 4 * cap, 8 * cap, 16 * cap}, len[4] = {4 * m, 4 * m, 8 * m, 8 * m};
+    unsigned char* const dst = c->h_rec;
+    const unsigned char* const src = c->rec_dev.p;
+    hipEvent_t ev = c->rec_ev;
+    c->rec_th = std::thread([c, dst, src, ev, off, len] {
+      c->rec_th_rc = hipEventSynchronize(ev) != hipSuccess ? ZDL_EDEVICE : sdma_copy(dst, src, off, len);
+    });
+    return ZDL_OK;
+  }
   if (rec_dma()) {  // ZDL_REC_DMA=1 (A/B): hipMemcpyAsync into coarse-grained pinned memory
     for (size_t off : {(size_t)0, 4 * cap})
       HIP_TRY(c, hipMemcpyAsync(c->h_rec + off, c->rec_dev.p + off, m * 4, hipMemcpyDeviceToHost, c->stream));
@@ -3432,6 +3514,7 @@ static int link_sparse(zdl_ctx* c, zdl_links* out, const SparseTable* tab = null
   if (rc != ZDL_OK) return rc;
   const size_t cap = c->h_rec_cap;
   HIP_TRY(c, hipStreamSynchronize(c->stream));
+  if (const int wrc = rec_wait(c)) return wrc;
   rc = status_code(c, (uint32_t)c->h_meta[0]);
   if (rc != ZDL_OK) return rc;
   out->n = m;

@@ -4,6 +4,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdlib>
 #include <utility>
 
 namespace zdl {
@@ -197,6 +198,33 @@ __global__ void __launch_bounds__(RL_T) k_rl_cells(const uint32_t* __restrict__ 
   }
 }
 
+// The log's sort: rocprim's onesweep radix sort with RB bits a pass (the gfx950 default is 8:
+// four passes over C5's 28-bit keys). ZDL_SORT_BITS (A/B) picks 8, 10 or 11.
+template <unsigned RB>
+using LogSortCfg = ::rocprim::radix_sort_config<
+    ::rocprim::default_config, ::rocprim::default_config,
+    ::rocprim::radix_sort_onesweep_config<::rocprim::kernel_config<1024, 8>, ::rocprim::kernel_config<1024, 8>, RB,
+                                          ::rocprim::block_radix_rank_algorithm::match>>;
+int sort_bits() {
+  static const int b = [] {
+    const char* e = getenv("ZDL_SORT_BITS");
+    const int v = e ? atoi(e) : 8;
+    return v == 10 || v == 11 ? v : 8;
+  }();
+  return b;
+}
+hipError_t sort_log(void* tmp, size_t& bytes, const uint32_t* in, uint32_t* out, uint64_t E, int key_bits,
+                    hipStream_t s) {
+  switch (sort_bits()) {
+    case 10:
+      return ::rocprim::radix_sort_keys<LogSortCfg<10>>(tmp, bytes, in, out, (size_t)E, 0u, (unsigned)key_bits, s);
+    case 11:
+      return ::rocprim::radix_sort_keys<LogSortCfg<11>>(tmp, bytes, in, out, (size_t)E, 0u, (unsigned)key_bits, s);
+    default:
+      return hipcub::DeviceRadixSort::SortKeys(tmp, bytes, in, out, (int)E, 0, key_bits, s);
+  }
+}
+
 hipError_t scratch(SparseWork& w, size_t need) {
   if (need <= w.tmp_bytes) return hipSuccess;
   if (w.tmp) (void)hipFree(w.tmp);
@@ -338,11 +366,11 @@ hipError_t sparse_accumulate(SparseWork& w, SparseTable& t, uint32_t* log, uint6
   uint32_t* const to = tc + nc;
   uint64_t* const Rd = w.d_count + 1;
   size_t a = 0, b = 0;
-  STRY(hipcub::DeviceRadixSort::SortKeys(nullptr, a, log, w.keys, (int)E, 0, key_bits, s));
+  STRY(sort_log(nullptr, a, log, w.keys, E, key_bits, s));
   STRY(hipcub::DeviceScan::ExclusiveSum(nullptr, b, tc, to, (int)nc, s));
   STRY(scratch(w, std::max(a, b)));
   size_t bytes = w.tmp_bytes;
-  STRY(hipcub::DeviceRadixSort::SortKeys(w.tmp, bytes, log, w.keys, (int)E, 0, key_bits, s));
+  STRY(sort_log(w.tmp, bytes, log, w.keys, E, key_bits, s));
   hipLaunchKernelGGL((k_rl_count<0, RL_PK>), dim3(nt), dim3(RL_T), 0, s, (const uint32_t*)w.keys,
                      (const uint64_t*)nullptr, E, tc);
   STRY(hipGetLastError());
