@@ -139,3 +139,29 @@ def test_gpu_daily_sorted_and_large_vs_cpp():
         got = sorted(zip(p[m].tolist(), c[m].tolist(), n[m].tolist(), e[m].tolist()))
         assert got == sorted(zip(op.tolist(), oc.tolist(), on.tolist(), oe.tolist()))
     assert sorted(days.tolist()) == sorted(set(trace_day.tolist()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(4))
+def test_gpu_daily_sparse_day_ranges(seed, monkeypatch):
+    """Days far apart (and one trace whose micros-vs-millis quirk floors it to 1970) are
+    linked by several contexts, each over a bounded range of the days present; the result
+    keeps aggregateLinks' first-seen day order."""
+    from zipkin_amd import daily
+    monkeypatch.setattr(daily, "TABLE_BUDGET_BYTES", 16 * 67 * 67 * 3)  # at most 3 days a context
+    r = random.Random(70 + seed)
+    base = 1_704_067_200_000_000
+    out = []
+    for k in range(80):
+        t = random_trace(r, allow_npe=False)
+        tid = format(r.getrandbits(64) | 1, "016x")
+        day = r.choice([0, 1, 2, 40, 41, 300, 301, 302, 303])
+        for s in t:
+            out.append(s.to_builder(trace_id=tid, timestamp=base + day * DAY * 1000 + r.randrange(DAY * 1000)))
+    q = random_trace(r, n=3, allow_npe=False)  # span 2 is 5 s after the epoch: the trace floors to 0
+    out += [s.to_builder(trace_id="00000000000000e1", timestamp=ts)
+            for s, ts in zip(q, [base, 5_000_000, base + 7])]
+    r.shuffle(out)
+    got = daily.aggregate_links(out)
+    assert _as_lists(got) == _as_lists(O.aggregate_links(out))
+    assert 0 in got and len(got) >= 8

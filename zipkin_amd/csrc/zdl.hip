@@ -1436,6 +1436,65 @@ __global__ void k_merge_compact(const unsigned long long* __restrict__ tcall, co
   ofirst[w] = tfirst[i];
 }
 
+// Insertion order, tables of at most MAP_CAP cells: the non-empty cells (first rank set) with
+// their counts and first ranks written straight into mapped pinned host memory (meta[0] the
+// status, meta[1] the count, then parent, child, call, err, first columns of MAP_CAP each) by
+// one workgroup, so link() costs one kernel and one wait; the host orders the records by rank.
+__global__ void __launch_bounds__(COMPACT_WG) k_ord_compact(const unsigned long long* __restrict__ tcall,
+                                                            const unsigned long long* __restrict__ terr,
+                                                            const unsigned long long* __restrict__ tfirst, uint32_t SS,
+                                                            uint32_t S, const uint32_t* __restrict__ status,
+                                                            unsigned long long* __restrict__ meta) {
+  __shared__ uint32_t wsum[COMPACT_WG / 64 + 1];
+  constexpr int KMAX = 8;
+  const uint32_t K = (SS + COMPACT_WG - 1) / COMPACT_WG, c0 = threadIdx.x * K;
+  unsigned long long fv[KMAX];
+  uint32_t nz = 0;
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) {
+    fv[k] = (uint32_t)k < K && c0 + k < SS ? tfirst[c0 + k] : ~0ull;
+    nz += fv[k] != ~0ull ? 1u : 0u;
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t incl = nz;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += y;
+  }
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+    for (int i = 0; i < COMPACT_WG / 64; ++i) {
+      const uint32_t t = wsum[i];
+      wsum[i] = acc;
+      acc += t;
+    }
+    meta[0] = *status;
+    meta[1] = acc;
+  }
+  __syncthreads();
+  unsigned char* b = reinterpret_cast<unsigned char*>(meta) + 16;
+  int32_t* op = reinterpret_cast<int32_t*>(b);
+  int32_t* oc = reinterpret_cast<int32_t*>(b + 4 * MAP_CAP);
+  int64_t* ocall = reinterpret_cast<int64_t*>(b + 8 * MAP_CAP);
+  int64_t* oerr = reinterpret_cast<int64_t*>(b + 16 * MAP_CAP);
+  uint64_t* ofirst = reinterpret_cast<uint64_t*>(b + 24 * MAP_CAP);
+  uint32_t o = wsum[w] + incl - nz;
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) {
+    if (fv[k] == ~0ull) continue;
+    const uint32_t i = c0 + k;
+    op[o] = (int32_t)(i / S);
+    oc[o] = (int32_t)(i % S);
+    ocall[o] = (int64_t)tcall[i];
+    oerr[o] = (int64_t)terr[i];
+    ofirst[o] = fv[k];
+    ++o;
+  }
+}
+
 }  // namespace zdl
 
 // ====================================================================== host
@@ -1598,6 +1657,8 @@ struct zdl_ctx {
   DevBuf<ZLink> o_links;
   uint64_t* h_meta = nullptr;  // pinned: link count, status
   unsigned long long* h_map = nullptr;  // mapped pinned: status, count, ordered records
+  unsigned long long* h_ordmap = nullptr;  // mapped pinned: insertion order's records (k_ord_compact)
+  unsigned long long* d_ordmap = nullptr;
   unsigned long long* d_map = nullptr;  // its device address
   bool map_fresh = false;               // h_map holds the compaction of the current table
   bool poisoned = false;                // a put stopped between its kernels: zdl_reset required
@@ -1618,6 +1679,8 @@ struct zdl_ctx {
   std::thread rec_th;
   int rec_th_rc = 0;
   hipEvent_t rec_ev = nullptr;
+  bool rec_job = false;  // a record copy is pending (run by rec_wait, or by rec_th once launched)
+  size_t rec_off[4] = {}, rec_len[4] = {};
   DevBuf<uint64_t> o_first;
   DevBuf<int32_t> mi_p, mi_c;
   DevBuf<int64_t> mi_call, mi_err;
@@ -1899,7 +1962,8 @@ void zdl_destroy(zdl_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)resolve_lazy(c, false);
   stage_free(c);
-  (void)rec_wait(c);
+  if (c->rec_th.joinable()) c->rec_th.join();  // a started link's copy; a pending one is dropped
+  c->rec_job = false;
   if (c->rec_ev) (void)hipEventDestroy(c->rec_ev);
   c->red_call.release();
   c->red_err.release();
@@ -1973,6 +2037,7 @@ void zdl_destroy(zdl_ctx* c) {
   c->o_links.release();
   if (c->h_meta) (void)hipHostFree(c->h_meta);
   if (c->h_map) (void)hipHostFree(c->h_map);
+  if (c->h_ordmap) (void)hipHostFree(c->h_ordmap);
   if (c->h_flag) (void)hipHostFree(c->h_flag);
   if (c->h_rec) (void)hipHostFree(c->h_rec);
   c->rec_dev.release();
@@ -3203,6 +3268,46 @@ static void sort_output(zdl_ctx* c, size_t n) {
 static int link_insertion(zdl_ctx* c, zdl_links* out, const unsigned long long* call,
                           const unsigned long long* errc, const unsigned long long* first_rank) {
   const uint64_t SS = (uint64_t)c->rows * c->S;
+  if (SS <= MAP_CAP) {  // one kernel into mapped memory, one wait, the rank sort on the host
+    if (!c->h_ordmap) {
+      HIP_TRY(c, hipHostMalloc((void**)&c->h_ordmap, 16 + 32 * MAP_CAP, hipHostMallocMapped | hipHostMallocCoherent));
+      HIP_TRY(c, hipHostGetDevicePointer((void**)&c->d_ordmap, c->h_ordmap, 0));
+    }
+    hipLaunchKernelGGL(k_ord_compact, dim3(1), dim3(COMPACT_WG), 0, c->stream, call, errc, first_rank, (uint32_t)SS,
+                       c->S, c->status.p, c->d_ordmap);
+    HIP_TRY(c, hipGetLastError());
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    put_times(c);
+    const int rc = status_code(c, (uint32_t)c->h_ordmap[0]);
+    if (rc != ZDL_OK) return rc;
+    const size_t m = (size_t)c->h_ordmap[1];
+    const unsigned char* b = reinterpret_cast<const unsigned char*>(c->h_ordmap) + 16;
+    const int32_t* p = reinterpret_cast<const int32_t*>(b);
+    const int32_t* ch = reinterpret_cast<const int32_t*>(b + 4 * MAP_CAP);
+    const int64_t* ca = reinterpret_cast<const int64_t*>(b + 8 * MAP_CAP);
+    const int64_t* er = reinterpret_cast<const int64_t*>(b + 16 * MAP_CAP);
+    const uint64_t* fr = reinterpret_cast<const uint64_t*>(b + 24 * MAP_CAP);
+    std::vector<std::pair<uint64_t, uint32_t>> key(m);
+    for (size_t i = 0; i < m; ++i) key[i] = {fr[i], (uint32_t)i};
+    std::sort(key.begin(), key.end());
+    c->out_p.resize(m);
+    c->out_c.resize(m);
+    c->out_call.resize(m);
+    c->out_err.resize(m);
+    for (size_t i = 0; i < m; ++i) {
+      const uint32_t j = key[i].second;
+      c->out_p[i] = p[j];
+      c->out_c[i] = ch[j];
+      c->out_call[i] = ca[j];
+      c->out_err[i] = er[j];
+    }
+    out->n = m;
+    out->parent = c->out_p.data();
+    out->child = c->out_c.data();
+    out->call_count = c->out_call.data();
+    out->error_count = c->out_err.data();
+    return ZDL_OK;
+  }
   HIP_TRY(c, c->o_p.ensure(SS));
   HIP_TRY(c, c->o_c.ensure(SS));
   HIP_TRY(c, c->o_call.ensure(SS));
@@ -3438,28 +3543,53 @@ static int sdma_copy(unsigned char* dst, const unsigned char* src, const size_t*
   return rc;
 }
 
+// The pending record copy: waited for (its helper thread) or, when no thread took it (a
+// synchronous zdl_link), run here - the compaction's event, then the SDMA copies.
 static int rec_wait(zdl_ctx* c) {
-  if (!c->rec_th.joinable()) return ZDL_OK;
-  c->rec_th.join();
-  const int rc = c->rec_th_rc;
-  c->rec_th_rc = ZDL_OK;
+  int rc = ZDL_OK;
+  if (c->rec_th.joinable()) {
+    c->rec_th.join();
+    rc = c->rec_th_rc;
+    c->rec_th_rc = ZDL_OK;
+  } else if (c->rec_job) {
+    rc = hipEventSynchronize(c->rec_ev) != hipSuccess ? ZDL_EDEVICE
+                                                      : sdma_copy(c->h_rec, c->rec_dev.p, c->rec_off, c->rec_len);
+  }
+  c->rec_job = false;
   return rc == ZDL_OK ? ZDL_OK : fail(c, rc, "SDMA copy of the link records failed");
+}
+
+// zdl_link_start: the pending record copy goes to a helper thread, so that it crosses PCIe
+// while the caller goes on (the next put); zdl_link_finish joins it.
+static int rec_launch(zdl_ctx* c) {
+  if (!c->rec_job || c->rec_th.joinable()) return ZDL_OK;
+  unsigned char* const dst = c->h_rec;
+  const unsigned char* const src = c->rec_dev.p;
+  hipEvent_t ev = c->rec_ev;
+  size_t off[4], len[4];
+  for (int k = 0; k < 4; ++k) {
+    off[k] = c->rec_off[k];
+    len[k] = c->rec_len[k];
+  }
+  c->rec_th = std::thread([c, dst, src, ev, off, len] {
+    c->rec_th_rc = hipEventSynchronize(ev) != hipSuccess ? ZDL_EDEVICE : sdma_copy(dst, src, off, len);
+  });
+  return ZDL_OK;
 }
 
 static int rec_download(zdl_ctx* c, uint64_t m) {
   const size_t cap = c->h_rec_cap;
   if (m == 0) return ZDL_OK;
-  if (rec_sdma()) {  // ZDL_REC_SDMA=1: a helper thread waits for the compaction, then SDMA
+  if (rec_sdma()) {  // SDMA: the copy job behind the compaction's event (rec_wait / rec_launch)
+    if (const int wrc = rec_wait(c)) return wrc;
     if (!c->rec_ev) HIP_TRY(c, hipEventCreateWithFlags(&c->rec_ev, hipEventDisableTiming));
     HIP_TRY(c, hipEventRecord(c->rec_ev, c->stream));
-    if (const int wrc = rec_wait(c)) return wrc;
     const size_t off[4] = {0, 4 * cap, 8 * cap, 16 * cap}, len[4] = {4 * m, 4 * m, 8 * m, 8 * m};
-    unsigned char* const dst = c->h_rec;
-    const unsigned char* const src = c->rec_dev.p;
-    hipEvent_t ev = c->rec_ev;
-    c->rec_th = std::thread([c, dst, src, ev, off, len] {
-      c->rec_th_rc = hipEventSynchronize(ev) != hipSuccess ? ZDL_EDEVICE : sdma_copy(dst, src, off, len);
-    });
+    for (int k = 0; k < 4; ++k) {
+      c->rec_off[k] = off[k];
+      c->rec_len[k] = len[k];
+    }
+    c->rec_job = true;
     return ZDL_OK;
   }
   if (rec_dma()) {  // ZDL_REC_DMA=1 (A/B): hipMemcpyAsync into coarse-grained pinned memory
@@ -3575,7 +3705,8 @@ int zdl_link_start(zdl_ctx* c, int order) {
   c->link_async = false;
   if (c->sparse && !c->comm && c->sub.empty() && order == ZDL_ORDER_SORTED && !c->poisoned) {
     HIP_TRY(c, enter(c));
-    const int rc = link_sparse_start(c, c->acc);
+    int rc = link_sparse_start(c, c->acc);
+    if (rc == ZDL_OK) rc = rec_launch(c);  // the records cross PCIe on an SDMA engine meanwhile
     if (rc != ZDL_OK) {
       c->link_pending = -1;
       return rc;

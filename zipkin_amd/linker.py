@@ -26,6 +26,7 @@ text whenever a node has one fragment).
 """
 from __future__ import annotations
 
+import functools
 import logging
 from typing import Iterable, List, Optional, Sequence
 
@@ -34,6 +35,8 @@ import numpy as np
 from . import _native as N
 from .columnar import Columns, Dictionary, pack_traces
 from .model import DependencyLink, Span
+
+_MAKE_LINK = functools.partial(tuple.__new__, DependencyLink)
 
 DENSE_MAX = 67         # S*S <= 4544 (WDENSE_MAX): k_link counts in its dense LDS table
 DENSE_MAX_WINDOW = 50  # S*S <= 2560 (WDENSE_MAX_WINDOW): the same with a time window
@@ -215,8 +218,9 @@ class DependencyLinker:
             return []
         p, c, n, e = self._ctx.link(self._order())
         low = self.svc.lowered()  # DependencyLink.Builder lower-cases (DependencyLink.java:72-82)
-        return [DependencyLink(low[a], low[b], x, y) for a, b, x, y in zip(p.tolist(), c.tolist(), n.tolist(),
-                                                                          e.tolist())]
+        # built without a Python frame per link (tuple.__new__ through a partial)
+        return list(map(_MAKE_LINK, zip(map(low.__getitem__, p.tolist()), map(low.__getitem__, c.tolist()),
+                                        n.tolist(), e.tolist())))
 
     @staticmethod
     def merge(links: Iterable[DependencyLink], device: int = 0) -> List[DependencyLink]:
