@@ -624,7 +624,7 @@ def main():
     doff = torch.from_numpy(cols.offsets.view(np.int64)).to(dev)
     ptrs = {k: v.data_ptr() for k, v in dcols.items()}
     ptrs["timestamp"] = None
-    inflight = args.inflight or (2 if world == 1 else 1)
+    inflight = args.inflight or 2
     # every in-flight context links its OWN copy of the batch (C2: 448 MB each), so a second
     # reader of the same bytes cannot be served from the 256 MiB Infinity Cache; the
     # shared-input step is measured beside it (config.ms_per_step_shared_input)
@@ -639,28 +639,30 @@ def main():
         keep.append(batches[-1][1])
     torch.cuda.synchronize(dev)
 
-    # HIP events around k_link on every 8th put of the timed region (each event pair costs
-    # the step a few microseconds)
-    ctx = N.Context(S, device=local, timing=True, timing_stride=args.timing_stride)
-    combine = "none"
-    if world > 1:
-        # libzdl joins one RCCL communicator (zdl_comm_init): zdl_link sums every rank's tables
-        # with ncclAllReduce over xGMI inside the library, as a JVM caller would get it. There is
-        # no other combine path: a rank that cannot join fails the run.
-        uid = [N.Context.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        try:
-            ctx.comm_init(uid[0], rank, world)
-        except N.ZdlError as ex:
-            log(f"[rank {rank}] zdl_comm_init failed: {ex}")
-            sys.exit(1)
-        combine = "libzdl RCCL all-reduce (zdl_comm_init)"
     # Steps in flight: with 2, step k+1's reset and put (another context, its own stream) are
     # enqueued before step k's links are read, so the host's work of reading one step's links
     # and launching the next overlaps the GPU's work instead of idling it (~25 us a step at C2).
-    # Every step still resets, links every span and reads every link back.
-    ctxs = [ctx] + [N.Context(S, device=local, timing=True, timing_stride=args.timing_stride)
-                    for _ in range(inflight - 1)]
+    # Every step still resets, links every span and reads every link back. HIP events time
+    # k_link on every timing_stride-th put (each event pair costs the step a few microseconds).
+    ctxs = [N.Context(S, device=local, timing=True, timing_stride=args.timing_stride)
+            for _ in range(inflight)]
+    ctx = ctxs[0]
+    combine = "none"
+    if world > 1:
+        # Every in-flight context joins its own RCCL communicator (zdl_comm_init): zdl_link sums
+        # every rank's tables with ncclAllReduce over xGMI inside the library, as a JVM caller
+        # would get it. The contexts' links are read one at a time in the same order on every
+        # rank (link() returns after its all-reduce), so the communicators' collectives never
+        # overlap. There is no other combine path: a rank that cannot join fails the run.
+        uids = [[N.Context.comm_unique_id() for _ in range(inflight)] if rank == 0 else None]
+        dist.broadcast_object_list(uids, src=0)
+        try:
+            for c, uid in zip(ctxs, uids[0]):
+                c.comm_init(uid, rank, world)
+        except N.ZdlError as ex:
+            log(f"[rank {rank}] zdl_comm_init failed: {ex}")
+            sys.exit(1)
+        combine = f"libzdl RCCL all-reduce (zdl_comm_init, one communicator per in-flight context x{inflight})"
 
     def launch(c, j=0):
         bp, bo = batches[j]
