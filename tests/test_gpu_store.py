@@ -160,10 +160,13 @@ def _index_cols(r, n, n_lo, n_ts):
 
 
 @pytest.mark.parametrize("seed,n,n_lo,n_ts", [(0, 2000, 50, 5), (1, 50_000, 3000, 40), (2, 400_000, 9000, 1000),
-                                              (3, 30_000, 1, 7), (4, 30_000, 30_000, 3)])
+                                              (3, 30_000, 1, 7), (4, 30_000, 30_000, 3),
+                                              (5, 40_000, 2000, 2 ** 40), (6, 40_000, 300, 2 ** 22)])
 def test_store_index_vs_numpy_restatement(seed, n, n_lo, n_ts):
     """zdl_store_evict / zdl_store_select against oracle/ims_index.py position for position,
-    over appends, evictions and compactions (which renumber the store)."""
+    over appends, evictions and compactions (which renumber the store). The timestamp ranges
+    take the selection's trace sort through its 0-bit (one trace), 32-bit and 64-bit key paths
+    (n_ts 2^40: keys wider than 32 bits); traces longer than 64 spans are placed by k_place_big."""
     from oracle import ims_index as X
     r = np.random.default_rng(seed)
     st = N.Store(0)

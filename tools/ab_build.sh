@@ -6,6 +6,6 @@ C=zipkin_amd/csrc
 while [ $# -ge 2 ]; do
   n=$1; d=$2; shift 2
   mkdir -p ab/$n
-  hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wno-unused-result -w $d $C/zdl.hip $C/zdl_group.hip $C/zdl_sparse.hip $C/zdl_proto3.hip $C/zdl_rows.hip $C/zdl_store.hip -o ab/$n/libzdl.so -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib &
+  hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wno-unused-result -w $d $C/zdl.hip $C/zdl_group.hip $C/zdl_sparse.hip $C/zdl_proto3.hip $C/zdl_rows.hip $C/zdl_store.hip -o ab/$n/libzdl.so -L/opt/rocm/lib -lrccl -lhsa-runtime64 -Wl,-rpath,/opt/rocm/lib &
 done
 wait

@@ -15,7 +15,7 @@ for d in ab/*/; do
   echo "$v serial(us k_link, step) $(j $O/abk1_$v.log)  inflight2 $(j $O/abk2_$v.log)"
 done
 done
-for d in ab/w*/; do
+for d in $(ls -d ab/w*/ 2>/dev/null); do
   v=$(basename $d)
   ZDL_PROF=1 ZDL_LIB_PATH=$PWD/$d/libzdl.so timeout -k 10 120 python -u $B --inflight 1 --steps 3 > $O/abkw_$v.log 2>&1 || exit $?
   echo "$v $(grep 'k_link waves' $O/abkw_$v.log)"

@@ -120,6 +120,87 @@ __global__ void k_runs(const uint64_t* __restrict__ key, uint64_t m, uint8_t* __
   if (i < m) flag[i] = i == 0 || key[i] != key[i - 1];
 }
 
+// flag[i] = the low id of span v[i] differs from v[i - 1]'s (v sorted by low id): k_take into a
+// key array and k_runs over it in one pass
+__global__ void k_runs_of(const uint64_t* __restrict__ lo, const uint32_t* __restrict__ v, uint64_t m,
+                          uint8_t* __restrict__ flag) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < m) flag[i] = i == 0 || lo[v[i]] != lo[v[i - 1]];
+}
+
+// ---- the set positions of flag[0..m) in order (offsets_of): a count pass and a write pass of
+// CF_TILE flags per workgroup (16 per thread, one 16-B load), the workgroups' starts from an
+// exclusive scan of the counts in between. (hipCUB's DeviceSelect::Flagged took 229 us for 10M
+// flags; these two passes read the flags twice, 20 MB.)
+constexpr int CF_WG = 256, CF_PER = 16, CF_TILE = CF_WG * CF_PER;
+
+// bit k: flag[i0 + k] != 0, k < 16
+__device__ __forceinline__ uint32_t flag_bits16(const uint8_t* __restrict__ flag, uint64_t i0, uint64_t m) {
+  uint32_t b = 0;
+  if (i0 + CF_PER <= m) {
+    const uint4 v = *reinterpret_cast<const uint4*>(flag + i0);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if ((w[q] >> (8 * k)) & 0xFFu) b |= 1u << (4 * q + k);
+  } else {
+    for (int k = 0; k < CF_PER; ++k)
+      if (i0 + (uint64_t)k < m && flag[i0 + k]) b |= 1u << k;
+  }
+  return b;
+}
+
+// exclusive prefix of x over the CF_WG threads; *total = the sum (call once per kernel)
+__device__ __forceinline__ uint32_t cf_scan(uint32_t x, uint32_t* total) {
+  __shared__ uint32_t ws[CF_WG / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t incl = x;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += y;
+  }
+  if (lane == 63) ws[w] = incl;
+  __syncthreads();
+  uint32_t before = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < CF_WG / 64; ++k) {
+    before += k < w ? ws[k] : 0u;
+    tot += ws[k];
+  }
+  *total = tot;
+  return before + incl - x;
+}
+
+__global__ void __launch_bounds__(CF_WG) k_flag_count(const uint8_t* __restrict__ flag, uint64_t m,
+                                                      uint32_t* __restrict__ cnt) {
+  const uint64_t i0 = ((uint64_t)blockIdx.x * CF_WG + threadIdx.x) * CF_PER;
+  uint32_t tot;
+  (void)cf_scan((uint32_t)__popc(flag_bits16(flag, i0, m)), &tot);
+  if (threadIdx.x == 0) cnt[blockIdx.x] = tot;
+}
+
+// start: the exclusive prefix of the workgroups' counts. The last workgroup also writes the
+// total into d[0] and m as the closing offset.
+__global__ void __launch_bounds__(CF_WG) k_flag_write(const uint8_t* __restrict__ flag, uint64_t m,
+                                                      const uint32_t* __restrict__ start, uint64_t* __restrict__ off,
+                                                      uint64_t* __restrict__ d) {
+  const uint64_t i0 = ((uint64_t)blockIdx.x * CF_WG + threadIdx.x) * CF_PER;
+  uint32_t bits = flag_bits16(flag, i0, m), tot;
+  uint64_t at = (uint64_t)start[blockIdx.x] + cf_scan((uint32_t)__popc(bits), &tot);
+  while (bits) {
+    off[at++] = i0 + (uint64_t)(__ffs(bits) - 1);
+    bits &= bits - 1u;
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
+    const uint64_t T = (uint64_t)start[blockIdx.x] + tot;
+    d[0] = T;
+    off[T] = m;
+  }
+}
+
 // flag[i] = a trace starts at position i of perm (low id changes; or high id, when given)
 // (alive: bit 1 = the trace id is 128-bit, normalized to 32 hex characters; with hi, the strict
 // grouping's key)
@@ -136,9 +217,6 @@ __global__ void k_trace_heads(const uint64_t* __restrict__ lo, const uint64_t* _
   flag[i] = h;
 }
 
-__global__ void k_close(uint64_t* __restrict__ off, const uint64_t* __restrict__ count, uint64_t m) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) off[*count] = m;
-}
 
 __global__ void k_widen(const uint8_t* __restrict__ flag, uint64_t m, uint32_t* __restrict__ out) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -160,16 +238,86 @@ __global__ void k_key_heads(const uint64_t* __restrict__ lo, const int64_t* __re
 }
 
 
+
+// the keys' smallest and largest value into d[2], d[3] (k_minmax_init first), so that the
+// sort runs over only the bits in which they differ
+__device__ __forceinline__ void key_minmax(uint64_t k, bool on, uint64_t* __restrict__ d) {
+  unsigned long long mn = on ? k : ~0ull, mx = on ? k : 0ull;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const unsigned long long a = __shfl_xor(mn, o, 64), b = __shfl_xor(mx, o, 64);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+  if ((threadIdx.x & 63) == 0 && mn <= mx) {
+    atomicMin(reinterpret_cast<unsigned long long*>(d + 2), mn);
+    atomicMax(reinterpret_cast<unsigned long long*>(d + 3), mx);
+  }
+}
+
+__global__ void k_minmax_init(uint64_t* __restrict__ d) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    d[1] = 0;
+    d[2] = ~0ull;
+    d[3] = 0;
+  }
+}
+
 // segment j's newest timestamp (the last span of j in v, sorted by timestamp inside a low id),
 // as a descending key; segments fed in reverse (descending low id) so a stable sort breaks
-// newest-timestamp ties by descending low id
-__global__ void k_seg_newest(const uint64_t* __restrict__ seg, uint64_t T, const uint32_t* __restrict__ v,
-                             const int64_t* __restrict__ ts, uint64_t* __restrict__ key, uint32_t* __restrict__ val) {
+// newest-timestamp ties by descending low id. The keys' range into d[2], d[3].
+__global__ void k_seg_newest_mm(const uint64_t* __restrict__ seg, uint64_t T, const uint32_t* __restrict__ v,
+                                const int64_t* __restrict__ ts, uint64_t* __restrict__ key, uint32_t* __restrict__ val,
+                                uint64_t* __restrict__ d) {
   const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= T) return;
-  const uint64_t newest = (uint64_t)ts[v[seg[j + 1] - 1]] ^ kSign;
-  key[T - 1 - j] = ~newest;
-  val[T - 1 - j] = (uint32_t)j;
+  uint64_t k = 0;
+  if (j < T) {
+    k = ~((uint64_t)ts[v[seg[j + 1] - 1]] ^ kSign);
+    key[T - 1 - j] = k;
+    val[T - 1 - j] = (uint32_t)j;
+  }
+  key_minmax(k, j < T, d);
+}
+
+// key - lo, as 32 bits (the range fits) or 64
+__global__ void k_key_rebase32(const uint64_t* __restrict__ key, uint64_t lo, uint64_t T, uint32_t* __restrict__ out) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < T) out[j] = (uint32_t)(key[j] - lo);
+}
+__global__ void k_key_rebase64(uint64_t* __restrict__ key, uint64_t lo, uint64_t T) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < T) key[j] -= lo;
+}
+
+// trace of rank r (order[r] = its segment j) copied to its new place start[r] of perm. A thread
+// per trace; a trace longer than PLACE_SMALL spans is listed (d[1] counts) for k_place_big.
+constexpr uint64_t PLACE_SMALL = 64;
+__global__ void k_place_seg(const uint32_t* __restrict__ v, const uint64_t* __restrict__ seg,
+                            const uint32_t* __restrict__ order, const uint32_t* __restrict__ start, uint64_t T,
+                            uint32_t* __restrict__ perm, uint32_t* __restrict__ big, uint64_t* __restrict__ d) {
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= T) return;
+  const uint32_t j = order[r];
+  const uint64_t b = seg[j], e = seg[j + 1];
+  if (e - b > PLACE_SMALL) {
+    big[atomicAdd(reinterpret_cast<unsigned long long*>(d + 1), 1ull)] = (uint32_t)r;
+    return;
+  }
+  uint32_t* out = perm + start[r];
+  for (uint64_t k = b; k < e; ++k) out[k - b] = v[k];
+}
+
+// the listed long traces, a workgroup each (grid-stride over the list)
+__global__ void k_place_big(const uint32_t* __restrict__ v, const uint64_t* __restrict__ seg,
+                            const uint32_t* __restrict__ order, const uint32_t* __restrict__ start,
+                            uint32_t* __restrict__ perm, const uint32_t* __restrict__ big, const uint64_t* __restrict__ d) {
+  const uint64_t nb = d[1];
+  for (uint64_t q = blockIdx.x; q < nb; q += gridDim.x) {
+    const uint32_t r = big[q], j = order[r];
+    const uint64_t b = seg[j], e = seg[j + 1];
+    uint32_t* out = perm + start[r];
+    for (uint64_t k = b + threadIdx.x; k < e; k += blockDim.x) out[k - b] = v[k];
+  }
 }
 
 // segment j's smallest timestamp (eviction order key); segments come in ascending low id
@@ -194,15 +342,6 @@ __global__ void k_rank_of(const uint32_t* __restrict__ order, uint64_t T, uint32
   if (r < T) rank[order[r]] = (uint32_t)r;
 }
 
-// moves span i of segment j (segid1 = j + 1) to its segment's new place
-__global__ void k_place(const uint32_t* __restrict__ v, const uint32_t* __restrict__ segid1,
-                        const uint64_t* __restrict__ seg, const uint32_t* __restrict__ rank,
-                        const uint32_t* __restrict__ start, uint64_t m, uint32_t* __restrict__ perm) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= m) return;
-  const uint32_t j = segid1[i] - 1;
-  perm[start[rank[j]] + (i - seg[j])] = v[i];
-}
 
 __global__ void k_new_off(const uint32_t* __restrict__ start, uint64_t T, uint64_t m, uint64_t* __restrict__ off) {
   const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -277,6 +416,7 @@ hipError_t reserve(IndexWork& w, uint64_t n) {
   for (auto*& p : w.sv) ITRY(grow(p, n));
   ITRY(grow(w.seg, n + 1));
   ITRY(grow(w.flag, n));
+  ITRY(grow(w.bc, 2 * (n / CF_TILE + 2)));
   w.cap = n;
   return hipSuccess;
 }
@@ -304,9 +444,9 @@ hipError_t fetch(IndexWork& w, int k, hipStream_t s) {
 }
 
 hipError_t sort64(IndexWork& w, const uint64_t* kin, uint64_t* kout, const uint32_t* vin, uint32_t* vout,
-                  uint64_t m, hipStream_t s) {
+                  uint64_t m, hipStream_t s, int end_bit = 64) {
   return cub_at(w, s, __LINE__, [&](void* t, size_t& b) {
-    return hipcub::DeviceRadixSort::SortPairs(t, b, kin, kout, vin, vout, (int)m, 0, 64, s);
+    return hipcub::DeviceRadixSort::SortPairs(t, b, kin, kout, vin, vout, (int)m, 0, end_bit, s);
   });
 }
 
@@ -332,11 +472,14 @@ hipError_t sum_scan(IndexWork& w, const uint32_t* in, uint32_t* out, uint64_t m,
 
 // the run heads of flag[0..m) as CSR offsets (off[0..T], T into w.d[0]); returns T
 hipError_t offsets_of(IndexWork& w, const uint8_t* flag, uint64_t m, uint64_t* off, uint64_t* T, hipStream_t s) {
+  const uint64_t nb = (m + CF_TILE - 1) / CF_TILE;  // m >= 1
+  hipLaunchKernelGGL(k_flag_count, dim3((unsigned)nb), dim3(CF_WG), 0, s, flag, m, w.bc);
+  ITRY(step_done(s, __LINE__));
   ITRY(cub_at(w, s, __LINE__, [&](void* t, size_t& b) {
-    return hipcub::DeviceSelect::Flagged(t, b, hipcub::CountingInputIterator<uint64_t>(0), flag, off, w.d, (int)m, s);
+    return hipcub::DeviceScan::ExclusiveSum(t, b, w.bc, w.bc + nb, (int)nb, s);
   }));
-  hipLaunchKernelGGL(k_close, dim3(1), dim3(64), 0, s, off, w.d, m);
-  ITRY(hipGetLastError());
+  hipLaunchKernelGGL(k_flag_write, dim3((unsigned)nb), dim3(CF_WG), 0, s, flag, m, w.bc + nb, off, w.d);
+  ITRY(step_done(s, __LINE__));
   ITRY(fetch(w, 1, s));
   *T = w.h[0];
   return hipSuccess;
@@ -352,6 +495,7 @@ void IndexWork::release() {
   for (auto*& p : sv) { if (p) (void)hipFree(p); p = nullptr; }
   if (seg) (void)hipFree(seg);
   if (flag) (void)hipFree(flag);
+  if (bc) (void)hipFree(bc);
   if (tmp) (void)hipFree(tmp);
   if (d) (void)hipFree(d);
   if (h) (void)hipHostFree(h);
@@ -362,6 +506,7 @@ void IndexWork::release() {
   ni = 0;
   seg = nullptr;
   flag = nullptr;
+  bc = nullptr;
   tmp = nullptr;
   d = nullptr;
   h = nullptr;
@@ -479,32 +624,55 @@ hipError_t index_select(IndexWork& w, const uint64_t* lo, const uint64_t* hi, co
   ITRY(index_update(w, lo, ts, n, s));  // accept keeps it current: normally nothing to do
   ITRY(reserve(w, n));  // before any w buffer is named: reserve reallocates them
   if (n == 0 || n_alive == 0) return hipSuccess;
-  uint32_t* const stored = w.v[1];  // low ids ascending, storage order inside (IMS:448-454)
-  uint32_t* const by_key = w.u[3];  // (low id, timestamp, arrival): the newest timestamps below
-  ITRY(alive_of(w, w.st, alive, n, n_alive, stored, &m, s));
-  if (m == 0) return hipSuccess;
-  uint64_t m2 = 0;
-  if (mode == SEL_NEWEST) {
-    ITRY(alive_of(w, w.bk, alive, n, n_alive, by_key, &m2, s));
-    if (m2 != m) return hipErrorUnknown;
+  // low ids ascending, storage order inside (IMS:448-454); (low id, timestamp, arrival) for the
+  // newest timestamps below. Nothing evicted: the resident orders themselves (no copy).
+  const uint32_t* stored = w.st;
+  const uint32_t* by_key = w.bk;
+  if (n_alive != n) {
+    ITRY(alive_of(w, w.st, alive, n, n_alive, w.v[1], &m, s));
+    stored = w.v[1];
+  } else {
+    m = n;
   }
-  LAUNCH(k_take, m, lo, stored, 0ull, w.k[1], m);  // their low ids
+  if (m == 0) return hipSuccess;
+  if (mode == SEL_NEWEST && n_alive != n) {
+    uint64_t m2 = 0;
+    ITRY(alive_of(w, w.bk, alive, n, n_alive, w.u[3], &m2, s));
+    if (m2 != m) return hipErrorUnknown;
+    by_key = w.u[3];
+  }
   uint64_t T = 0;
   if (mode == SEL_ALL) {
     ITRY(hipMemcpyAsync(perm, stored, m * 4, hipMemcpyDeviceToDevice, s));
-    LAUNCH(k_runs, m, w.k[1], m, w.flag);
+    LAUNCH(k_runs_of, m, lo, stored, m, w.flag);
     ITRY(offsets_of(w, w.flag, m, off, &T, s));
   } else if (mode == SEL_NEWEST) {
-    LAUNCH(k_runs, m, w.k[1], m, w.flag);
+    LAUNCH(k_runs_of, m, lo, stored, m, w.flag);
     ITRY(offsets_of(w, w.flag, m, w.seg, &T, s));  // the same low-id segments in by_key and stored
-    LAUNCH(k_seg_newest, T, w.seg, T, by_key, ts, w.sk[0], w.sv[0]);
-    ITRY(sort64(w, w.sk[0], w.sk[1], w.sv[0], w.sv[1], T, s));
+    // one key per trace (its newest timestamp, descending), sorted over the bits in which the
+    // keys differ: 32-bit keys when their range fits (a selection of under ~71 minutes of
+    // microsecond timestamps), the 64-bit ones from that range's top bit down otherwise
+    hipLaunchKernelGGL(k_minmax_init, dim3(1), dim3(64), 0, s, w.d);
+    LAUNCH(k_seg_newest_mm, T, w.seg, T, by_key, ts, w.sk[0], w.sv[0], w.d);
+    ITRY(fetch(w, 4, s));
+    const uint64_t klo = w.h[2], span = w.h[3] - w.h[2];
+    const int bits = span == 0 ? 0 : 64 - __builtin_clzll(span);
+    if (bits == 0) {  // one key: the stable order is the input order
+      ITRY(hipMemcpyAsync(w.sv[1], w.sv[0], T * 4, hipMemcpyDeviceToDevice, s));
+    } else if (bits <= 32) {
+      LAUNCH(k_key_rebase32, T, w.sk[0], klo, T, w.u[0]);
+      ITRY(sort32(w, w.u[0], w.u[1], w.sv[0], w.sv[1], T, s, bits));
+    } else {
+      LAUNCH(k_key_rebase64, T, w.sk[0], klo, T);
+      ITRY(sort64(w, w.sk[0], w.sk[1], w.sv[0], w.sv[1], T, s, bits));
+    }
+    // the traces' new starts, then each trace's span run copied there (k_minmax_init zeroed
+    // the long-trace count d[1])
     LAUNCH(k_seg_sizes, T, w.seg, w.sv[1], T, w.u[0]);
     ITRY(sum_scan(w, w.u[0], w.u[1], T, false, s));
-    LAUNCH(k_rank_of, T, w.sv[1], T, w.sv[0]);
-    LAUNCH(k_widen, m, w.flag, m, w.u[2]);
-    ITRY(sum_scan(w, w.u[2], w.u[0], m, true, s));
-    LAUNCH(k_place, m, stored, w.u[0], w.seg, w.sv[0], w.u[1], m, perm);
+    LAUNCH(k_place_seg, T, stored, w.seg, w.sv[1], w.u[1], T, perm, w.u[2], w.d);
+    hipLaunchKernelGGL(k_place_big, dim3(256), dim3(256), 0, s, stored, w.seg, w.sv[1], w.u[1], perm, w.u[2], w.d);
+    ITRY(step_done(s, __LINE__));
     LAUNCH(k_new_off, T + 1, w.u[1], T, m, off);
   } else if (mode == SEL_ALL_STRICT) {
     // group by (low id, trace id) - the normalized id string: its high 64 bits and its width,

@@ -37,6 +37,7 @@ struct IndexWork {
   uint64_t* sk[2] = {};  // segment-level sort keys
   uint32_t* sv[2] = {};  // segment-level sort values
   uint8_t* flag = nullptr;
+  uint32_t* bc = nullptr;  // offsets_of: per-workgroup flag counts, then their exclusive prefix
   uint64_t* d = nullptr;  // device scalars [4]
   uint64_t* h = nullptr;  // pinned host scalars [4]
   size_t cap = 0;
