@@ -42,6 +42,7 @@ constexpr int BIG_WG = 1024;        // threads per big-trace workgroup
 constexpr int HCAP = 2048;          // LDS hash slots of the (parent, child) table when S*S is large
 constexpr int HPROBE = 4;   // LDS hash probes before an add goes straight to HBM
 constexpr int WSMALL = 64;          // traces up to this many spans are k_link's
+constexpr uint32_t ORD_RANK_ONLY = 1u << 15;  // Args::skip: wave_link ranks addLinks, counts nothing
 constexpr int TAIL_WG = 1024;       // threads per k_tail workgroup (= BIG_WG)
 constexpr int WDENSE_MAX = 4544;    // S*S <= this -> dense u64 LDS cells (call | err << 32): S <= 67
 constexpr int WTABLE_BYTES = 36864; // max(8 * (WDENSE_MAX + 64 dummy cells), 12 * HCAP); two k_link
@@ -103,9 +104,11 @@ struct Args {
                              // k_tail (which the put then does not launch), else stores seq | FLAG_TAIL
   unsigned long long* prof;  // ZDL_PROF=1: k_link phase cycles (12 counters)
   uint64_t* cx_win;      // k_link -> k_tail: (base | P << 48, starts mask) per window
+  uint32_t cx_slots;     // cx_win holds a slot per trace (k_link mode 3), not a queue of cx_count
   uint32_t skip;         // timing-only ablation of k_link (ZDL_SKIP): 32 stream only, 64 fields,
                          // 128 +hash, 256 +parents, 512 +jumping, 2048 no table adds, 4096 cache-resident;
-                         // k_tail insertion order: 8192 no breadth-first ranks, 16384 no ord_min
+                         // k_tail insertion order: 8192 no breadth-first ranks, 16384 no ord_min;
+                         // ORD_RANK_ONLY (zdl_ord.inc's pass): ranks without counts
   // big-trace scratch (HBM), indexed by global span index
   uint64_t* b_id;
   uint64_t* b_pid;
@@ -1392,6 +1395,8 @@ inline const void* k_tail_fn(int dense, int window, int ord = 0) {  // dense: 0 
   return window ? (const void*)k_tail<0, 1, 0> : (const void*)k_tail<0, 0, 0>;
 }
 
+#include "zdl_ord.inc"  // insertion order's second pass after a mode 6 put
+
 // Any S: non-zero cells -> records in arbitrary order (the host sorts them).
 __global__ void k_compact(const unsigned long long* __restrict__ call, const unsigned long long* __restrict__ err,
                           uint64_t SS, uint32_t S, unsigned long long* __restrict__ count, ZLink* __restrict__ out) {
@@ -1572,6 +1577,7 @@ struct zdl_ctx {
   std::vector<unsigned long long> h_day_first;
   std::vector<int64_t> out_day, out_days;
   DevBuf<unsigned long long> first, o_key;
+  DevBuf<uint64_t> ord_n;  // insertion order, mode 6: the traces zdl_ord.inc's pass ranks
 
   uint64_t span_base = 0;
   DevBuf<uint32_t> o_fa, o_fb, o_bfs;
@@ -1916,6 +1922,12 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
       for (int o = 0; o < 2 && e == hipSuccess; ++o)
         e = hipFuncSetAttribute(k_tail_fn(d, w, o), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)tail_block_bytes(w));
+  for (int w = 0; w < 2 && e == hipSuccess; ++w) {
+    e = hipFuncSetAttribute(k_link_fn(TM_DENSE, w, 6), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)link_block_bytes(w, TM_DENSE, 6));
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute(k_ord_rank_fn(w), hipFuncAttributeMaxDynamicSharedMemorySize, (int)tail_block_bytes(w));
+  }
   if (e == hipSuccess) {
     const char* pe = getenv("ZDL_PROF");
     c->prof_on = pe && pe[0] == '1';
@@ -1972,7 +1984,7 @@ void zdl_destroy(zdl_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (auto& r : c->rank) r.release();
   c->call.release(); c->errc.release(); c->status.release();
-  c->first.release(); c->day_first.release(); c->o_key.release(); c->o_fa.release(); c->o_fb.release(); c->o_bfs.release();
+  c->first.release(); c->ord_n.release(); c->day_first.release(); c->o_key.release(); c->o_fa.release(); c->o_fb.release(); c->o_bfs.release();
   c->big_list.release(); c->big_stat.release(); c->big_exact_list.release(); c->counters.release(); c->retry.release();
   c->cx_win.release();
   if (c->prof_on && c->prof.p) {
@@ -2483,9 +2495,15 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   A.small_max = WSMALL;
   A.cx_count = ctr + CTR_CX;
   A.cx_win = c->cx_win.p;
+  A.cx_slots = plan_only ? 1u : 0u;
   A.skip = c->skip;
   A.prof = c->prof.p;
-  const int lmode = plan_only ? 3 : c->ord ? 4 : (c->flags & ZDL_FLAG_TREE_STREAM) ? 5 : (c->prof_on ? 1 : (c->skip ? 2 : 0));
+  // insertion order: mode 6 (first traces, then zdl_ord.inc's pass) on dense tables, mode 4
+  // (every simple window ranked in k_link) otherwise: other tables, ZDL_FLAG_TREE_STREAM (its
+  // breadth-first indexes come from mode 4's), or ZDL_ORD_MODE4=1 (A/B)
+  static const bool ord_mode4 = getenv("ZDL_ORD_MODE4") != nullptr;
+  const int omode = tm == TM_DENSE && !ord_mode4 && !(c->flags & ZDL_FLAG_TREE_STREAM) ? 6 : 4;
+  const int lmode = plan_only ? 3 : c->ord ? omode : (c->flags & ZDL_FLAG_TREE_STREAM) ? 5 : (c->prof_on ? 1 : (c->skip ? 2 : 0));
   const uint32_t lW = (uint32_t)lgrid * (uint32_t)lk::waves(c->window, lmode);  // k_link's waves
   const uint32_t lP = (uint32_t)((SS + (1u << PSHIFT) - 1) >> PSHIFT);
   if (tm == TM_SORT) {  // k_link's segments in [0, 2n), k_tail's in [2n, 4n)
@@ -2580,6 +2598,7 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
     c->tr_n = n_spans;
   }
   if (c->ord) {
+    HIP_TRY(c, c->ord_n.ensure(1));
     HIP_TRY(c, c->o_key.ensure(n_spans));
     HIP_TRY(c, c->o_fa.ensure(n_spans));
     HIP_TRY(c, c->o_fb.ensure(n_spans));
@@ -2677,6 +2696,23 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
     return hip_fail(c, le, "k_tail launch");
   }
   if (A.map) c->seq = A.seq;
+  if (lmode == 6) {  // the placeholders' traces ranked exactly (zdl_ord.inc); cx_win is free again
+    hipLaunchKernelGGL(k_ord_winners, dim3(1), dim3(OW_WG), 0, c->stream, c->first.p, (uint32_t)SS, off, n_traces,
+                       n_traces_dev, c->span_base, n_spans, c->cx_win.p, c->ord_n.p, c->status.p);
+    Args R = A;
+    R.n_traces_dev = c->ord_n.p;
+    R.cx_slots = 1;
+    R.skip = A.skip | ORD_RANK_ONLY;
+    void* rargs[] = {&R};
+    hipError_t oe = hipGetLastError();
+    if (oe == hipSuccess)
+      oe = hipLaunchKernel(k_ord_rank_fn(c->window), dim3(grid), dim3(TAIL_WG), rargs, tail_block_bytes(c->window),
+                           c->stream);
+    if (oe != hipSuccess) {
+      c->poisoned = true;  // the counts are in, the ranks are not
+      return hip_fail(c, oe, "insertion order pass launch");
+    }
+  }
   ev_record(c, 4);
   if (c->sparse) {  // gather the put's log segments, sort, reduce and merge into the list
     const int rc = sparse_finish(c, ep, lW, n_spans, n_traces, off);
