@@ -128,6 +128,8 @@ struct Args {
   // insertion order (ZDL_FLAG_INSERTION_ORDER): first-addLink ranks per cell (ord_min),
   // the put-global position of this put's span 0, and big-trace breadth-first scratch
   unsigned long long* first;
+  unsigned long long* ord_w;  // insertion order, mode 6: per cell the put's first simple trace
+                              // adding it, (start << 8 | length), put-relative (zdl_ord.inc)
   uint64_t span_base;
   // daily buckets (zdl_set_days): rows = days * S (else S), day 0 = midnight day0 (ms);
   // day_first[d] = put-global position of day d's first trace
@@ -1578,6 +1580,7 @@ struct zdl_ctx {
   std::vector<int64_t> out_day, out_days;
   DevBuf<unsigned long long> first, o_key;
   DevBuf<uint64_t> ord_n;  // insertion order, mode 6: the traces zdl_ord.inc's pass ranks
+  DevBuf<unsigned long long> ord_w;  // ... and the first simple trace of each pair (Args::ord_w)
 
   uint64_t span_base = 0;
   DevBuf<uint32_t> o_fa, o_fb, o_bfs;
@@ -1984,7 +1987,7 @@ void zdl_destroy(zdl_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (auto& r : c->rank) r.release();
   c->call.release(); c->errc.release(); c->status.release();
-  c->first.release(); c->ord_n.release(); c->day_first.release(); c->o_key.release(); c->o_fa.release(); c->o_fb.release(); c->o_bfs.release();
+  c->first.release(); c->ord_n.release(); c->ord_w.release(); c->day_first.release(); c->o_key.release(); c->o_fa.release(); c->o_fb.release(); c->o_bfs.release();
   c->big_list.release(); c->big_stat.release(); c->big_exact_list.release(); c->counters.release(); c->retry.release();
   c->cx_win.release();
   if (c->prof_on && c->prof.p) {
@@ -2599,11 +2602,13 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   }
   if (c->ord) {
     HIP_TRY(c, c->ord_n.ensure(1));
+    HIP_TRY(c, c->ord_w.ensure(SS));
     HIP_TRY(c, c->o_key.ensure(n_spans));
     HIP_TRY(c, c->o_fa.ensure(n_spans));
     HIP_TRY(c, c->o_fb.ensure(n_spans));
     HIP_TRY(c, c->o_bfs.ensure(n_spans));
     A.first = c->first.p;
+    A.ord_w = c->ord_w.p;
     A.span_base = c->span_base;
     A.o_key = c->o_key.p;
     A.o_fa = c->o_fa.p;
@@ -2624,6 +2629,7 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   static const bool nolazy = getenv("ZDL_NOLAZY") != nullptr;
   A.lazy = A.map && tm == TM_DENSE && lmode == 0 && !nolazy && !(c->flags & ZDL_FLAG_TIMING_ALL) ? 1 : 0;
   void* kargs[] = {&A};
+  if (lmode == 6) HIP_TRY(c, hipMemsetAsync(c->ord_w.p, 0xFF, SS * 8, c->stream));  // no pair recorded yet
   ev_record(c, 0);
   ev_record(c, 1);
   // A failed launch poisons nothing yet either: no kernel of this put ran
@@ -2697,8 +2703,8 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   }
   if (A.map) c->seq = A.seq;
   if (lmode == 6) {  // the placeholders' traces ranked exactly (zdl_ord.inc); cx_win is free again
-    hipLaunchKernelGGL(k_ord_winners, dim3(1), dim3(OW_WG), 0, c->stream, c->first.p, (uint32_t)SS, off, n_traces,
-                       n_traces_dev, c->span_base, n_spans, c->cx_win.p, c->ord_n.p, c->status.p);
+    hipLaunchKernelGGL(k_ord_winners, dim3(1), dim3(OW_WG), 0, c->stream, c->ord_w.p, (uint32_t)SS, n_spans,
+                       c->cx_win.p, c->ord_n.p, c->status.p);
     Args R = A;
     R.n_traces_dev = c->ord_n.p;
     R.cx_slots = 1;

@@ -444,13 +444,6 @@ __device__ __forceinline__ void ord_min(unsigned long long* f, unsigned long lon
 __device__ __forceinline__ unsigned long long ord_rank(uint64_t trace_pos, uint32_t bfs, int k) {
   return ((unsigned long long)trace_pos << 24) | ((unsigned long long)bfs << 1) | (unsigned long long)k;
 }
-// k_link mode 6: the position of a pair's first trace with every low bit set, which no rank has
-// (breadth-first indexes stay below 2^21); zdl_ord.inc ranks that trace's links exactly after
-// the put, and the smaller exact rank replaces it
-constexpr unsigned long long ORD_PH = 0xFFFFFFull;
-__device__ __forceinline__ unsigned long long ord_placeholder(uint64_t trace_pos) {
-  return ((unsigned long long)trace_pos << 24) | ORD_PH;
-}
 
 // Daily buckets (ITDependencies.aggregateLinks, ITDependencies.java:666-700): a trace's day
 // is flooredTraceTimestamp's, restated literally over its spans in storage order: the first

@@ -239,9 +239,11 @@ __global__ void k_key_heads(const uint64_t* __restrict__ lo, const int64_t* __re
 
 
 
-// the keys' smallest and largest value into d[2], d[3] (k_minmax_init first), so that the
-// sort runs over only the bits in which they differ
-__device__ __forceinline__ void key_minmax(uint64_t k, bool on, uint64_t* __restrict__ d) {
+// The keys' smallest and largest value: each workgroup's pair into part[blockIdx.x] and
+// part[nb + blockIdx.x], then k_minmax_final into d[2], d[3] (one atomic per wave on two
+// addresses serialised at the memory side: 368 us for 1M keys)
+__device__ __forceinline__ void key_minmax(uint64_t k, bool on, uint64_t* __restrict__ part) {
+  __shared__ unsigned long long wmn[4], wmx[4];
   unsigned long long mn = on ? k : ~0ull, mx = on ? k : 0ull;
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) {
@@ -249,26 +251,59 @@ __device__ __forceinline__ void key_minmax(uint64_t k, bool on, uint64_t* __rest
     mn = a < mn ? a : mn;
     mx = b > mx ? b : mx;
   }
-  if ((threadIdx.x & 63) == 0 && mn <= mx) {
-    atomicMin(reinterpret_cast<unsigned long long*>(d + 2), mn);
-    atomicMax(reinterpret_cast<unsigned long long*>(d + 3), mx);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    wmn[w] = mn;
+    wmx[w] = mx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < (int)(blockDim.x >> 6); ++i) {
+      mn = wmn[i] < mn ? wmn[i] : mn;
+      mx = wmx[i] > mx ? wmx[i] : mx;
+    }
+    part[blockIdx.x] = mn;
+    part[gridDim.x + blockIdx.x] = mx;
   }
 }
 
-__global__ void k_minmax_init(uint64_t* __restrict__ d) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) {
-    d[1] = 0;
-    d[2] = ~0ull;
-    d[3] = 0;
+__global__ void __launch_bounds__(1024) k_minmax_final(const uint64_t* __restrict__ part, uint64_t nb,
+                                                       uint64_t* __restrict__ d) {
+  __shared__ unsigned long long wmn[16], wmx[16];
+  unsigned long long mn = ~0ull, mx = 0ull;
+  for (uint64_t i = threadIdx.x; i < nb; i += blockDim.x) {
+    mn = part[i] < mn ? part[i] : mn;
+    mx = part[nb + i] > mx ? part[nb + i] : mx;
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const unsigned long long a = __shfl_xor(mn, o, 64), b = __shfl_xor(mx, o, 64);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+  if ((threadIdx.x & 63) == 0) {
+    wmn[threadIdx.x >> 6] = mn;
+    wmx[threadIdx.x >> 6] = mx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < 16; ++i) {
+      mn = wmn[i] < mn ? wmn[i] : mn;
+      mx = wmx[i] > mx ? wmx[i] : mx;
+    }
+    d[1] = 0;  // k_place_seg's long-trace count
+    d[2] = mn;
+    d[3] = mx;
   }
 }
 
 // segment j's newest timestamp (the last span of j in v, sorted by timestamp inside a low id),
 // as a descending key; segments fed in reverse (descending low id) so a stable sort breaks
-// newest-timestamp ties by descending low id. The keys' range into d[2], d[3].
-__global__ void k_seg_newest_mm(const uint64_t* __restrict__ seg, uint64_t T, const uint32_t* __restrict__ v,
-                                const int64_t* __restrict__ ts, uint64_t* __restrict__ key, uint32_t* __restrict__ val,
-                                uint64_t* __restrict__ d) {
+// newest-timestamp ties by descending low id. Each workgroup's key range into part.
+__global__ void __launch_bounds__(256) k_seg_newest_mm(const uint64_t* __restrict__ seg, uint64_t T,
+                                                       const uint32_t* __restrict__ v, const int64_t* __restrict__ ts,
+                                                       uint64_t* __restrict__ key, uint32_t* __restrict__ val,
+                                                       uint64_t* __restrict__ part) {
   const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t k = 0;
   if (j < T) {
@@ -276,7 +311,7 @@ __global__ void k_seg_newest_mm(const uint64_t* __restrict__ seg, uint64_t T, co
     key[T - 1 - j] = k;
     val[T - 1 - j] = (uint32_t)j;
   }
-  key_minmax(k, j < T, d);
+  key_minmax(k, j < T, part);
 }
 
 // key - lo, as 32 bits (the range fits) or 64
@@ -289,22 +324,58 @@ __global__ void k_key_rebase64(uint64_t* __restrict__ key, uint64_t lo, uint64_t
   if (j < T) key[j] -= lo;
 }
 
-// trace of rank r (order[r] = its segment j) copied to its new place start[r] of perm. A thread
-// per trace; a trace longer than PLACE_SMALL spans is listed (d[1] counts) for k_place_big.
-constexpr uint64_t PLACE_SMALL = 64;
-__global__ void k_place_seg(const uint32_t* __restrict__ v, const uint64_t* __restrict__ seg,
-                            const uint32_t* __restrict__ order, const uint32_t* __restrict__ start, uint64_t T,
-                            uint32_t* __restrict__ perm, uint32_t* __restrict__ big, uint64_t* __restrict__ d) {
-  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= T) return;
-  const uint32_t j = order[r];
-  const uint64_t b = seg[j], e = seg[j + 1];
-  if (e - b > PLACE_SMALL) {
-    big[atomicAdd(reinterpret_cast<unsigned long long*>(d + 1), 1ull)] = (uint32_t)r;
-    return;
+// The traces of ranks [256 b, 256 b + 256) (order[r] = its segment j) copied to their new places
+// start[r] of perm: each thread claims its trace's slots of the workgroup's span run in an LDS
+// owner map, then the run is copied span-parallel (writes coalesced, reads in the traces'
+// runs). A trace longer than PLACE_SMALL spans is listed (d[1] counts) for k_place_big. (A
+// thread per trace copying its own spans took 115 us for C2's 1M traces: every lane of an
+// access in another line.)
+constexpr int PL_WG = 256;
+constexpr uint32_t PLACE_SMALL = 64;
+__global__ void __launch_bounds__(PL_WG) k_place_seg(const uint32_t* __restrict__ v, const uint64_t* __restrict__ seg,
+                                                     const uint32_t* __restrict__ order,
+                                                     const uint32_t* __restrict__ start, uint64_t T,
+                                                     uint32_t* __restrict__ perm, uint32_t* __restrict__ big,
+                                                     uint64_t* __restrict__ d) {
+  __shared__ uint32_t pre[PL_WG], src[PL_WG], dst[PL_WG], ws[PL_WG / 64];
+  __shared__ uint8_t owner[PL_WG * PLACE_SMALL];
+  const uint64_t r = (uint64_t)blockIdx.x * PL_WG + threadIdx.x;
+  uint32_t sz = 0;
+  if (r < T) {
+    const uint32_t j = order[r];
+    const uint64_t b = seg[j], e = seg[j + 1];
+    if (e - b > PLACE_SMALL) {
+      big[atomicAdd(reinterpret_cast<unsigned long long*>(d + 1), 1ull)] = (uint32_t)r;
+    } else {
+      sz = (uint32_t)(e - b);
+      src[threadIdx.x] = (uint32_t)b;
+      dst[threadIdx.x] = start[r];
+    }
   }
-  uint32_t* out = perm + start[r];
-  for (uint64_t k = b; k < e; ++k) out[k - b] = v[k];
+  // exclusive prefix of the sizes over the workgroup
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t incl = sz;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) ws[w] = incl;
+  __syncthreads();
+  uint32_t before = 0, total = 0;
+#pragma unroll
+  for (int k = 0; k < PL_WG / 64; ++k) {
+    before += k < w ? ws[k] : 0u;
+    total += ws[k];
+  }
+  const uint32_t p0 = before + incl - sz;
+  pre[threadIdx.x] = p0;
+  for (uint32_t k = 0; k < sz; ++k) owner[p0 + k] = (uint8_t)threadIdx.x;
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < total; i += PL_WG) {
+    const uint32_t q = owner[i], k = i - pre[q];
+    perm[dst[q] + k] = v[src[q] + k];
+  }
 }
 
 // the listed long traces, a workgroup each (grid-stride over the list)
@@ -652,8 +723,8 @@ hipError_t index_select(IndexWork& w, const uint64_t* lo, const uint64_t* hi, co
     // one key per trace (its newest timestamp, descending), sorted over the bits in which the
     // keys differ: 32-bit keys when their range fits (a selection of under ~71 minutes of
     // microsecond timestamps), the 64-bit ones from that range's top bit down otherwise
-    hipLaunchKernelGGL(k_minmax_init, dim3(1), dim3(64), 0, s, w.d);
-    LAUNCH(k_seg_newest_mm, T, w.seg, T, by_key, ts, w.sk[0], w.sv[0], w.d);
+    LAUNCH(k_seg_newest_mm, T, w.seg, T, by_key, ts, w.sk[0], w.sv[0], w.sk[1]);
+    hipLaunchKernelGGL(k_minmax_final, dim3(1), dim3(1024), 0, s, w.sk[1], (uint64_t)grid_of(T).x, w.d);
     ITRY(fetch(w, 4, s));
     const uint64_t klo = w.h[2], span = w.h[3] - w.h[2];
     const int bits = span == 0 ? 0 : 64 - __builtin_clzll(span);
@@ -666,11 +737,13 @@ hipError_t index_select(IndexWork& w, const uint64_t* lo, const uint64_t* hi, co
       LAUNCH(k_key_rebase64, T, w.sk[0], klo, T);
       ITRY(sort64(w, w.sk[0], w.sk[1], w.sv[0], w.sv[1], T, s, bits));
     }
-    // the traces' new starts, then each trace's span run copied there (k_minmax_init zeroed
+    // the traces' new starts, then each trace's span run copied there (k_minmax_final zeroed
     // the long-trace count d[1])
     LAUNCH(k_seg_sizes, T, w.seg, w.sv[1], T, w.u[0]);
     ITRY(sum_scan(w, w.u[0], w.u[1], T, false, s));
-    LAUNCH(k_place_seg, T, stored, w.seg, w.sv[1], w.u[1], T, perm, w.u[2], w.d);
+    hipLaunchKernelGGL(k_place_seg, dim3((unsigned)((T + PL_WG - 1) / PL_WG)), dim3(PL_WG), 0, s, stored, w.seg, w.sv[1],
+                       w.u[1], T, perm, w.u[2], w.d);
+    ITRY(step_done(s, __LINE__));
     hipLaunchKernelGGL(k_place_big, dim3(256), dim3(256), 0, s, stored, w.seg, w.sv[1], w.u[1], perm, w.u[2], w.d);
     ITRY(step_done(s, __LINE__));
     LAUNCH(k_new_off, T + 1, w.u[1], T, m, off);
