@@ -130,6 +130,10 @@ struct Args {
   unsigned long long* first;
   unsigned long long* ord_w;  // insertion order, mode 6: per cell the put's first simple trace
                               // adding it, (start << 8 | length), put-relative (zdl_ord.inc)
+  unsigned long long* ord_log;  // ... each wave's records (cell << 40 | start << 8 | length),
+  uint64_t* ord_start;          // its segment's start in ord_log and its record count
+  uint32_t* ord_cnt;
+  uint64_t ord_stride;          // segments at wave * ord_stride (0: at 2 x the chunk's first span)
   uint64_t span_base;
   // daily buckets (zdl_set_days): rows = days * S (else S), day 0 = midnight day0 (ms);
   // day_first[d] = put-global position of day d's first trace
@@ -1580,7 +1584,10 @@ struct zdl_ctx {
   std::vector<int64_t> out_day, out_days;
   DevBuf<unsigned long long> first, o_key;
   DevBuf<uint64_t> ord_n;  // insertion order, mode 6: the traces zdl_ord.inc's pass ranks
-  DevBuf<unsigned long long> ord_w;  // ... and the first simple trace of each pair (Args::ord_w)
+  DevBuf<unsigned long long> ord_w;  // ... and the first simple trace of each pair (Args::ord_w),
+  DevBuf<unsigned long long> ord_log, ord_part;  // the waves' records, k_ord_reduce's partials
+  DevBuf<uint64_t> ord_start;
+  DevBuf<uint32_t> ord_cnt;
 
   uint64_t span_base = 0;
   DevBuf<uint32_t> o_fa, o_fb, o_bfs;
@@ -1987,7 +1994,8 @@ void zdl_destroy(zdl_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (auto& r : c->rank) r.release();
   c->call.release(); c->errc.release(); c->status.release();
-  c->first.release(); c->ord_n.release(); c->ord_w.release(); c->day_first.release(); c->o_key.release(); c->o_fa.release(); c->o_fb.release(); c->o_bfs.release();
+  c->first.release(); c->ord_n.release(); c->ord_w.release(); c->ord_log.release(); c->ord_part.release();
+  c->ord_start.release(); c->ord_cnt.release(); c->day_first.release(); c->o_key.release(); c->o_fa.release(); c->o_fb.release(); c->o_bfs.release();
   c->big_list.release(); c->big_stat.release(); c->big_exact_list.release(); c->counters.release(); c->retry.release();
   c->cx_win.release();
   if (c->prof_on && c->prof.p) {
@@ -2603,6 +2611,21 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   if (c->ord) {
     HIP_TRY(c, c->ord_n.ensure(1));
     HIP_TRY(c, c->ord_w.ensure(SS));
+    if (lmode == 6) {
+      if ((lW + ORD_RED_G - 1) / ORD_RED_G > (uint32_t)ORD_RED_MAXW)
+        return fail(c, ZDL_EINVAL, "insertion order: too many k_link waves for k_ord_reduce");
+      // a wave records at most two pairs a span, and with its bitset of the cells seen at most
+      // every cell once
+      const uint64_t full = LK_ORD6_SEEN ? (uint64_t)lW * SS : ~0ull;
+      A.ord_stride = 2 * n_spans <= full ? 0 : SS;
+      HIP_TRY(c, c->ord_log.ensure(std::max<uint64_t>(1, std::min<uint64_t>(2 * n_spans, full))));
+      HIP_TRY(c, c->ord_start.ensure(lW));
+      HIP_TRY(c, c->ord_cnt.ensure(lW));
+      HIP_TRY(c, c->ord_part.ensure((size_t)ORD_RED_G * SS));
+      A.ord_log = c->ord_log.p;
+      A.ord_start = c->ord_start.p;
+      A.ord_cnt = c->ord_cnt.p;
+    }
     HIP_TRY(c, c->o_key.ensure(n_spans));
     HIP_TRY(c, c->o_fa.ensure(n_spans));
     HIP_TRY(c, c->o_fb.ensure(n_spans));
@@ -2629,7 +2652,6 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   static const bool nolazy = getenv("ZDL_NOLAZY") != nullptr;
   A.lazy = A.map && tm == TM_DENSE && lmode == 0 && !nolazy && !(c->flags & ZDL_FLAG_TIMING_ALL) ? 1 : 0;
   void* kargs[] = {&A};
-  if (lmode == 6) HIP_TRY(c, hipMemsetAsync(c->ord_w.p, 0xFF, SS * 8, c->stream));  // no pair recorded yet
   ev_record(c, 0);
   ev_record(c, 1);
   // A failed launch poisons nothing yet either: no kernel of this put ran
@@ -2702,7 +2724,11 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
     return hip_fail(c, le, "k_tail launch");
   }
   if (A.map) c->seq = A.seq;
-  if (lmode == 6) {  // the placeholders' traces ranked exactly (zdl_ord.inc); cx_win is free again
+  if (lmode == 6) {  // the pairs' first simple traces ranked exactly (zdl_ord.inc); cx_win is free again
+    hipLaunchKernelGGL(k_ord_reduce, dim3(ORD_RED_G), dim3(ORD_RED_WG), (size_t)SS * 8, c->stream, c->ord_log.p,
+                       c->ord_start.p, c->ord_cnt.p, lW, (uint32_t)SS, c->ord_part.p);
+    hipLaunchKernelGGL(k_ord_final, dim3((unsigned)((SS + 255) / 256)), dim3(256), 0, c->stream, c->ord_part.p,
+                       (uint32_t)SS, c->ord_w.p);
     hipLaunchKernelGGL(k_ord_winners, dim3(1), dim3(OW_WG), 0, c->stream, c->ord_w.p, (uint32_t)SS, n_spans,
                        c->cx_win.p, c->ord_n.p, c->status.p);
     Args R = A;

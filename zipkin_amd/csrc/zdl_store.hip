@@ -514,17 +514,23 @@ hipError_t fetch(IndexWork& w, int k, hipStream_t s) {
   return hipStreamSynchronize(s);
 }
 
+// rocprim's radix sort, onesweep at every size above one block: its default config switches to
+// a merge sort up to 2^20 items (block sort + 20 merge passes: 190 us for 1M trace keys, against
+// tens of us for a few radix passes)
+using StoreSortCfg = ::rocprim::radix_sort_config<::rocprim::default_config, ::rocprim::default_config,
+                                                  ::rocprim::default_config, 0>;
+
 hipError_t sort64(IndexWork& w, const uint64_t* kin, uint64_t* kout, const uint32_t* vin, uint32_t* vout,
                   uint64_t m, hipStream_t s, int end_bit = 64) {
   return cub_at(w, s, __LINE__, [&](void* t, size_t& b) {
-    return hipcub::DeviceRadixSort::SortPairs(t, b, kin, kout, vin, vout, (int)m, 0, end_bit, s);
+    return ::rocprim::radix_sort_pairs<StoreSortCfg>(t, b, kin, kout, vin, vout, (size_t)m, 0u, (unsigned)end_bit, s);
   });
 }
 
 hipError_t sort32(IndexWork& w, const uint32_t* kin, uint32_t* kout, const uint32_t* vin, uint32_t* vout,
                   uint64_t m, hipStream_t s, int end_bit = 32) {
   return cub_at(w, s, __LINE__ * 64 + end_bit, [&](void* t, size_t& b) {
-    return hipcub::DeviceRadixSort::SortPairs(t, b, kin, kout, vin, vout, (int)m, 0, end_bit, s);
+    return ::rocprim::radix_sort_pairs<StoreSortCfg>(t, b, kin, kout, vin, vout, (size_t)m, 0u, (unsigned)end_bit, s);
   });
 }
 
