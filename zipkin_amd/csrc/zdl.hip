@@ -1238,7 +1238,8 @@ __device__ __forceinline__ void compact_ordered(const unsigned long long* __rest
 // queued window) it compacts the table into the mapped buffer, zeroes the next put's counter
 // slots and releases `seq` - the put is complete without launching them; otherwise it stores
 // seq | FLAG_TAIL and the host launches them (zdl_link, or the context's next call).
-__device__ void lk_lazy_end(const Args& A, uint32_t* scratch) {
+__device__ void lk_lazy_end(const Args& A0, uint32_t* scratch) {
+  KArgs& A = rare(A0);  // read here from the argument segment, not held across k_link's loop
   // scratch (LDS, after the table flush): [0] last, [1] tail, [4..] compact_ordered's sums
   uint32_t& last = scratch[0];
   uint32_t& tail = scratch[1];
