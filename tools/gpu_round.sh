@@ -16,7 +16,7 @@ timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smo
 timeout -k 10 300 python -u bench.py > $O/bench_$TAG.log 2>&1 || exit $?
 [ "$2" = "quick" ] && exit 0
 timeout -k 10 300 python -u bench.py --config c3 > $O/bench_c3_$TAG.log 2>&1 || exit $?
-B="bench.py --steps 10 --warmup 2 --inflight 1 --no-parity --no-cpu-baseline --no-proto3 --no-json --no-store --no-mysql-rows --no-insertion-order --no-h2d --no-c5 --no-traffic"
+B="bench.py --steps 10 --warmup 2 --inflight 1 --no-parity --no-cpu-baseline --no-proto3 --no-json --no-store --no-mysql-rows --no-insertion-order --no-h2d --no-c5 --no-traffic --no-put-trace"
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/prof_$TAG -o run --output-format csv -- python3 $B > $O/prof_${TAG}_bench.log 2>&1 || exit $?
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/prof_c3_$TAG -o run --output-format csv -- python3 $B --config c3 > $O/prof_c3_${TAG}_bench.log 2>&1 || exit $?
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch_$TAG -o run --output-format csv -- python3 $B > $O/pmc_fetch_$TAG.log 2>&1 || exit $?
