@@ -570,7 +570,7 @@ def main():
     ap.add_argument("--no-store", action="store_true", help="skip the resident-store getDependencies side leg")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 (high-cardinality) side leg")
     ap.add_argument("--no-put-trace", action="store_true", help="skip the per-trace putTrace loop side leg")
-    ap.add_argument("--c5-host-threads", type=int, default=1, choices=(1, 2),
+    ap.add_argument("--c5-host-threads", type=int, default=2, choices=(1, 2),
                     help="C5 leg: one host thread per context (2) or one alternating both (1)")
     ap.add_argument("--no-traffic", action="store_true",
                     help="skip the rocprofv3 FETCH_SIZE / WRITE_SIZE passes behind roofline.traffic")

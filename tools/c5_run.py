@@ -17,11 +17,12 @@ def main():
     ap.add_argument("--giant-min", default=None)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--host-threads", type=int, default=2, choices=(1, 2))
     a = ap.parse_args()
     if a.giant_min is not None:
         os.environ["ZDL_GIANT_MIN"] = str(a.giant_min)
     import bench
-    r = bench.c5_leg(0, steps=a.steps, parity=not a.no_parity)
+    r = bench.c5_leg(0, steps=a.steps, parity=not a.no_parity, host_threads=a.host_threads)
     print(json.dumps(r), flush=True)
 
 
