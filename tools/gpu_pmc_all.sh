@@ -20,7 +20,7 @@ run() {  # name timeout command...
 }
 B="bench.py --steps 3 --warmup 1 --inflight 1 --no-parity --no-cpu-baseline --no-traffic --no-c5"
 run c3 300 python3 $B --config c3 || exit $?
-run c5 400 python3 tools/c5_run.py --no-parity --steps 2 || exit $?
+run c5 400 python3 tools/c5_run.py --no-parity --steps 2 --host-threads 1 || exit $?
 run json 240 python3 tools/json_decode_run.py --reps 2 || exit $?
 run proto3 240 python3 tools/json_decode_run.py --reps 2 --format proto3 || exit $?
 exit 0

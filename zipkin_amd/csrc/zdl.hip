@@ -1644,6 +1644,8 @@ struct zdl_ctx {
   int giant_min = 2048;  // traces longer than this (ZDL_GIANT_MIN; 0: off, k_tail's workgroups)
   DevBuf<uint32_t> gg_bi, gg_n, gg_tile0, gg_bad, gg_tile_g, gg_bstart, gg_blen, gg_meta, gg_H, gg_rest;
   DevBuf<unsigned char> gg_tmp;
+  DevBuf<uint32_t> gg_part32;  // k_g_prep_*'s block sums, then carries
+  DevBuf<unsigned long long> gg_part64;
   DevBuf<uint64_t> gg_base, gg_h0;
   DevBuf<unsigned long long> gg_root, gg_tsroot, gg_tsmin;
   DevBuf<int32_t> gg_rootidx;
@@ -2047,6 +2049,8 @@ void zdl_destroy(zdl_ctx* c) {
                   &c->gg_meta, &c->gg_H, &c->gg_rest})
     b->release();
   c->gg_tmp.release();
+  c->gg_part32.release();
+  c->gg_part64.release();
   if (c->gg_ev) (void)hipEventDestroy(c->gg_ev);
   c->gg_base.release(); c->gg_h0.release(); c->gg_root.release(); c->gg_tsroot.release(); c->gg_tsmin.release();
   c->gg_rootidx.release(); c->gg_stat.release();
@@ -2282,7 +2286,7 @@ static int sparse_finish(zdl_ctx* c, uint32_t ep, uint32_t lW, uint64_t n_spans,
 }
 
 // The device-wide big-trace tier (zdl_giant.inc), sparse contexts only. giant_prep runs right
-// after k_link, before k_mid: k_g_prep splits k_link's back list on the device's own count of it
+// after k_link, before k_mid: k_g_prep_* split k_link's back list on the device's own count of it
 // and its totals are copied to pinned memory behind an event; giant_run (after k_mid's launch)
 // waits for that event only - k_mid keeps running meanwhile - and launches the tier's kernels,
 // which queue behind k_mid. Arrays indexed by back-list entry are sized by the bound on the
@@ -2335,7 +2339,13 @@ static int giant_prep(zdl_ctx* c, Args& A, uint64_t n_spans, uint64_t n_traces) 
   G.rest = c->gg_rest.p;
   G.nl = (uint32_t)nl;
   HIP_TRY(c, hipMemsetAsync(c->gg_meta.p, 0, GM_WORDS * 4, s));
-  hipLaunchKernelGGL(k_g_prep, dim3(1), dim3(GT), 0, s, A, G);
+  const uint32_t nb = (uint32_t)((nl + GT - 1) / GT);
+  HIP_TRY(c, c->gg_part32.ensure(4 * (size_t)nb));
+  HIP_TRY(c, c->gg_part64.ensure(nb));
+  hipLaunchKernelGGL(k_g_prep_count, dim3(nb), dim3(GT), 0, s, A, G, c->gg_part32.p, c->gg_part64.p);
+  hipLaunchKernelGGL(k_g_prep_scan, dim3(1), dim3(GT), 0, s, A, G, nb, c->gg_part32.p, c->gg_part64.p);
+  hipLaunchKernelGGL(k_g_prep_write, dim3(nb), dim3(GT), 0, s, A, G, (const uint32_t*)c->gg_part32.p,
+                     (const unsigned long long*)c->gg_part64.p);
   HIP_TRY(c, hipGetLastError());
   HIP_TRY(c, hipMemcpyAsync(c->h_gmeta, c->gg_meta.p, GM_WORDS * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(c, hipEventRecord(c->gg_ev, s));
