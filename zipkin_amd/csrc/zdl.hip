@@ -190,12 +190,10 @@ struct Args {
   uint32_t* exact_n;        // appended as found (k_tail walks this list, not the whole back list)
   uint32_t* tick_big;       // k_big's trace tickets
   uint32_t kb_small;        // k_big<256> takes the traces of at most this many spans (<= KB_SMALL)
-  uint32_t kb_mid;          // k_big<1024, 1> those above kb_small up to this many (= kb_small: no launch)
 };
 // The counter block of one put (two alternate by put, so no put issues a memset)
 enum : int { CTR_MID = 0, CTR_CX = 1, CTR_LARGE = 2, CTR_TICK_LARGE = 3, CTR_TICK_MID = 4, CTR_RETRY = 5,
-             CTR_TICK_BIG = 6, CTR_EXACT = 8, CTR_N = 10 };  // (CTR_TICK_BIG + 1: k_big<256>'s tickets,
-                                                              // + 3 (slot 9): k_big<1024, 1>'s)
+             CTR_TICK_BIG = 6, CTR_EXACT = 8, CTR_N = 10 };  // (CTR_TICK_BIG + 1: k_big<256>'s tickets)
 constexpr int CTR_DONE = 2 * CTR_N;  // k_tail's finished-workgroup count (after both blocks)
 
 #include "zdl_full.inc"  // the full per-window emulation (k_tail's first part)
@@ -1358,20 +1356,16 @@ __global__ void __launch_bounds__(TAIL_WG, 1) k_tail(Args A) {
 // 2 for k_tail's exact path.
 constexpr int KB_SMALL_LDS = 38400;
 constexpr int KB_SMALL = (KB_SMALL_LDS - 240) / 81;  // bs_bytes(n) <= KB_SMALL_LDS
-constexpr int KB_MID_LDS = 81920;
-constexpr int KB_MID = (KB_MID_LDS - 240) / 81;  // bs_bytes(n) <= KB_MID_LDS
-constexpr int KB_MID_WG = 768;  // two workgroups a CU: 6 waves a SIMD (<= 80 VGPRs)
 constexpr int KB_BATCH = 16;
-template <int NT, int CLS = NT == 256 ? 0 : 2>  // CLS: the size class this launch links
-__global__ void __launch_bounds__(NT, CLS == 0 ? 4 : CLS == 1 ? 6 : 1) k_big(Args A) {
+template <int NT>
+__global__ void __launch_bounds__(NT, NT == 256 ? 4 : 1) k_big(Args A) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   __shared__ uint32_t sh_j;
+  constexpr bool SMALL = NT == 256;
   const uint32_t nlarge = A.grest ? *A.grest_n : *A.large_count;
   if (nlarge == 0) return;
-  const size_t lds_bytes = CLS == 0 ? (size_t)KB_SMALL_LDS
-                           : CLS == 1 ? (size_t)KB_MID_LDS
-                                      : tail_block_bytes(A.days ? 2 : A.window);
-  uint32_t* const tick = A.tick_big + (CLS == 0 ? 1 : CLS == 1 ? 3 : 0);
+  const size_t lds_bytes = SMALL ? (size_t)KB_SMALL_LDS : tail_block_bytes(A.days ? 2 : A.window);
+  uint32_t* const tick = SMALL ? A.tick_big + 1 : A.tick_big;
   while (true) {
     __syncthreads();
     if (threadIdx.x == 0) sh_j = atomicAdd(tick, (uint32_t)KB_BATCH);
@@ -1382,8 +1376,7 @@ __global__ void __launch_bounds__(NT, CLS == 0 ? 4 : CLS == 1 ? 6 : 1) k_big(Arg
       const uint32_t bi = A.grest ? A.grest[j] : A.big_cap - 1u - j;
       const uint32_t t = A.big_list[bi];
       const uint64_t n = A.off[t + 1] - A.off[t];  // (k_link checked the offsets; a flagged trace
-      const int cls = n <= (uint64_t)A.kb_small ? 0 : n <= (uint64_t)A.kb_mid ? 1 : 2;  // (a flagged trace
-      if (cls != CLS) continue;  // has n out of range: the large launch's)
+      if (SMALL != (n <= (uint64_t)A.kb_small)) continue;  // has n out of range: the large launch's)
       const uint8_t gs = A.gstat ? A.gstat[bi] : 0;  // the giant tier's verdict (uniform)
       uint8_t st = gs;
       if (gs == 0) st = big_one<0, true, NT>(A, lds, lds_bytes, bi, true) ? 1 : 2;
@@ -1937,8 +1930,6 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
                             (int)std::max(tail_block_bytes(0), std::max(tail_block_bytes(1), tail_block_bytes(2))));
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)k_big<256>, hipFuncAttributeMaxDynamicSharedMemorySize, KB_SMALL_LDS);
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)k_big<KB_MID_WG, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, KB_MID_LDS);
   for (int d = 0; d < 2 && e == hipSuccess; ++d)
     for (int w = 0; w < 3 && e == hipSuccess; ++w)
       for (int o = 0; o < 2 && e == hipSuccess; ++o)
@@ -2397,14 +2388,10 @@ static int giant_run(zdl_ctx* c, Args& A) {
 // A lazy put's k_mid / k_tail, when its k_link left them work (flag seq | FLAG_TAIL) or has not
 // finished yet (then they run after it in stream order and find what there is; k_tail compacts
 // and releases seq again). wait: spin for k_link first (zdl_link); otherwise never waits.
-// k_big's launches (small traces, four workgroups per CU; sparse contexts: the middle class, two
-// a CU; then the longer ones)
-static int launch_big(zdl_ctx* c, void** kargs, const Args& A, int wmode) {
+// k_big's two launches (small traces, four workgroups per CU; then the longer ones)
+static int launch_big(zdl_ctx* c, void** kargs, int wmode) {
   hipError_t be = hipLaunchKernel((const void*)k_big<256>, dim3((unsigned)c->cus * 4), dim3(256), kargs,
                                   (size_t)KB_SMALL_LDS, c->stream);
-  if (be == hipSuccess && A.kb_mid > A.kb_small)
-    be = hipLaunchKernel((const void*)k_big<KB_MID_WG, 1>, dim3((unsigned)c->cus * 2), dim3(KB_MID_WG), kargs,
-                         (size_t)KB_MID_LDS, c->stream);
   if (be == hipSuccess)
     be = hipLaunchKernel((const void*)k_big<TAIL_WG>, dim3(c->grid), dim3(TAIL_WG), kargs, tail_block_bytes(wmode),
                          c->stream);
@@ -2441,7 +2428,7 @@ static int resolve_lazy(zdl_ctx* c, bool wait) {
     }
   }
   if (A.bstat) {
-    const int brc = launch_big(c, kargs, A, c->lazy_wmode);
+    const int brc = launch_big(c, kargs, c->lazy_wmode);
     if (brc != ZDL_OK) return brc;
   }
   const hipError_t le = hipLaunchKernel(k_tail_fn(c->lazy_dense, c->lazy_wmode, 0), dim3(c->grid), dim3(TAIL_WG), kargs,
@@ -2523,11 +2510,6 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
       return e ? (uint32_t)std::min<long>(std::max<long>(atol(e), 0), KB_SMALL) : (uint32_t)KB_SMALL;
     }();
     A.kb_small = kbs;
-    static const uint32_t kbm = [] {
-      const char* e = getenv("ZDL_KB_MID");  // A/B and tests: 0 = no middle class
-      return e ? (uint32_t)std::min<long>(std::max<long>(atol(e), 0), KB_MID) : (uint32_t)KB_MID;
-    }();
-    A.kb_mid = c->sparse && kbs > 0 ? std::max(kbs, kbm) : kbs;
   }
   A.ctr_next = c->counters.p + (ep ^ 1u) * CTR_N;
   A.big_cap = (uint32_t)n_traces;
@@ -2741,7 +2723,7 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   }
   ev_record(c, 8);
   if (A.bstat) {
-    const int brc = launch_big(c, kargs, A, wmode);
+    const int brc = launch_big(c, kargs, wmode);
     if (brc != ZDL_OK) return brc;
   }
   const hipError_t le = hipLaunchKernel(k_tail_fn(c->sparse ? 2 : dense, wmode, c->ord ? 1 : 0), dim3(grid),
