@@ -110,3 +110,55 @@ def test_native_put_trace_loop_c2_vs_cpp():
     assert st == 0
     got = sorted(zip(p.tolist(), c.tolist(), n.tolist(), e.tolist()))
     assert got == sorted(zip(op.tolist(), oc.tolist(), on.tolist(), oe.tolist()))
+
+
+@pytest.mark.parametrize("seed", range(4))
+@pytest.mark.parametrize("cap", ["300", "2000"])
+def test_lone_put_after_staged_big_traces_sorted(monkeypatch, seed, cap):
+    """Sorted order (the lazy k_mid / k_tail path): staged batches holding traces of 65-200
+    spans leave k_mid / k_tail deferred; a trace put alone right after (its merge may throw,
+    or it is longer than the staging slot) must not regrow or refill the columns those
+    deferred kernels read. Links equal the oracle's."""
+    monkeypatch.setenv("ZDL_STAGE_SPANS", cap)
+    r = random.Random(1300 + seed)
+    ol = O.DependencyLinker()
+    gl = DependencyLinker(insertion_order=False)
+    npes = 0
+    for i in range(120):
+        x = r.random()
+        if x < 0.3:
+            t = random_trace(r, n=r.randint(65, 200), allow_npe=False, id_pool=400)
+        elif x < 0.45:
+            t = random_trace(r, n=r.randint(2, 10))  # allow_npe: may go alone and may throw
+        elif x < 0.5:
+            t = random_trace(r, n=int(cap) + r.randint(1, 300), allow_npe=False, id_pool=4000)
+        else:
+            t = random_trace(r, n=r.randint(1, 30), allow_npe=False)
+        try:
+            ol.put_trace(t)
+            raised = False
+        except O.ReferenceNPE:
+            raised = True
+        if raised:
+            npes += 1
+            with pytest.raises(N.ReferenceNullPointerException):
+                gl.put_trace(t)
+        else:
+            gl.put_trace(t)
+    assert sorted(_as_list(gl.link())) == sorted(_as_list(ol.link()))
+    gl.close()
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_merge_runs_are_staged_and_linked(stage, seed):
+    """Traces with merge runs whose Trace.merge cannot throw (every non-null endpoint complete)
+    are staged like any other; the links (and insertion order) equal the oracle's."""
+    r = random.Random(1700 + seed)
+    traces = [random_trace(r, n=r.randint(2, 40), allow_npe=False, id_pool=3) for _ in range(200)]
+    ol = O.DependencyLinker()
+    gl = DependencyLinker()
+    for t in traces:
+        ol.put_trace(t)
+        gl.put_trace(t)
+    assert _as_list(gl.link()) == _as_list(ol.link())
+    gl.close()

@@ -201,6 +201,25 @@ def test_store_index_vs_numpy_restatement(seed, n, n_lo, n_ts):
     st.close()
 
 
+@pytest.mark.parametrize("n", [1, 2, 3, 257])
+def test_store_select_tiny_stores(n):
+    """Stores of a handful of spans: the selection's per-workgroup min / max partials
+    (k_seg_newest_mm, 2 per workgroup of traces) fit the scratch sized from the span count
+    (a one-span store wrote one past it)."""
+    from oracle import ims_index as X
+    r = np.random.default_rng(100 + n)
+    st = N.Store(0)
+    cols, lo, hi, ts = _index_cols(r, n, n, 5)
+    st.append(cols, hi)
+    alive = np.ones(n, bool)
+    for mode in (X.SELECT_NEWEST, X.SELECT_ALL, X.SELECT_ALL_STRICT):
+        perm, off = st.selection(mode)
+        want_perm, want_off = X.select(lo, hi, ts, alive, mode)
+        np.testing.assert_array_equal(off, want_off)
+        np.testing.assert_array_equal(perm, want_perm)
+    st.close()
+
+
 def test_store_index_link_matches_host_selection():
     """zdl_put_selection (device-resident selection) links what zdl_put_stored links for the
     same selection uploaded from the host."""

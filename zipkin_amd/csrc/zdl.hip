@@ -3166,6 +3166,10 @@ int zdl_put_selection(zdl_ctx* c, const zdl_store* st) {
   if (!st->sel_valid) return fail(c, ZDL_EINVAL, "zdl_put_selection: no current selection (zdl_store_select)");
   if (st->sel_traces == 0) return ZDL_OK;
   HIP_TRY(c, enter(c));
+  {  // a lazy put's k_mid / k_tail read the previous put's columns and scratch: launched first
+    const int lrc = resolve_lazy(c, false);
+    if (lrc != ZDL_OK) return lrc;
+  }
   HIP_TRY(c, hipStreamSynchronize(st->stream));
   return put_stored_dev(c, st, st->sel.p, st->sel_n, st->sel_off.p, st->sel_traces);
 }
@@ -3184,6 +3188,10 @@ int zdl_put_stored(zdl_ctx* c, const zdl_store* st, const uint32_t* perm, uint64
   for (uint64_t i = 0; i < n_sel; ++i)
     if (perm[i] >= st->n) return fail(c, ZDL_EINVAL, "zdl_put_stored: selection outside the store");
   HIP_TRY(c, enter(c));
+  {  // a lazy put's k_mid / k_tail read h_off / h_ord: launched before they are regrown or refilled
+    const int lrc = resolve_lazy(c, false);
+    if (lrc != ZDL_OK) return lrc;
+  }
   HIP_TRY(c, hipStreamSynchronize(st->stream));
   HIP_TRY(c, c->h_ord.ensure(n_sel));
   HIP_TRY(c, c->h_off.ensure(n_traces + 1));
@@ -3209,6 +3217,10 @@ int zdl_put_spans_device(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans,
   // larger input into several puts; the counts accumulate)
   if (n_traces >= 0xffffffffull || n_spans > (1ull << 32) - 129) return fail(c, ZDL_EINVAL, "input too large");
   HIP_TRY(c, enter(c));
+  {  // a lazy put's k_mid / k_tail read the previous put's columns and scratch: launched first
+    const int lrc = resolve_lazy(c, false);
+    if (lrc != ZDL_OK) return lrc;
+  }
   if (!off) return put_spans_ungrouped(c, col, n_spans);
   return put_spans_link(c, col, n_spans, off, n_traces);
 }
@@ -3246,6 +3258,10 @@ int zdl_put_spans(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans, const 
   }
   if (n_spans == 0) return ZDL_OK;
   HIP_TRY(c, enter(c));
+  {  // a lazy put's k_mid / k_tail read the h_* columns: launched before they are regrown or refilled
+    const int lrc = resolve_lazy(c, false);
+    if (lrc != ZDL_OK) return lrc;
+  }
   HIP_TRY(c, c->h_id.ensure(n_spans));
   HIP_TRY(c, c->h_pid.ensure(n_spans));
   HIP_TRY(c, c->h_lsvc.ensure(n_spans));

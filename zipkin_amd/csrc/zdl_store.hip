@@ -483,7 +483,8 @@ hipError_t reserve(IndexWork& w, uint64_t n) {
   for (auto*& p : w.k) ITRY(grow(p, n));
   for (auto*& p : w.v) ITRY(grow(p, n));
   for (auto*& p : w.u) ITRY(grow(p, n));
-  for (auto*& p : w.sk) ITRY(grow(p, n));
+  // sk[1] also holds k_seg_newest_mm's per-workgroup min / max partials (2 per 256 traces)
+  for (auto*& p : w.sk) ITRY(grow(p, std::max<uint64_t>(n, 2 * grid_of(n).x)));
   for (auto*& p : w.sv) ITRY(grow(p, n));
   ITRY(grow(w.seg, n + 1));
   ITRY(grow(w.flag, n));
