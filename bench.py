@@ -273,6 +273,49 @@ def put_trace_leg(cols, S, device, links, reps=3):
                     "columns, PCIe-inclusive; staged in pinned batches of 2^20 spans"}
 
 
+def put_trace_c4_leg(device, traces=1_000_000, reps=3):
+    """The same per-trace call pattern over C4 (messaging-heavy, 5 % of spans split into merge
+    fragments, duplicate ids, missing brokers): every trace through one zdl_put_trace. A trace
+    goes alone and synchronously only when its Trace.merge could throw (an (id, shared) group
+    holding a null and an incomplete endpoint, zdl_stage.inc); C4's splits never can, so every
+    trace is staged. Beside it: one DependencyLinker restated in C++ over the same batch on one
+    thread (the reference's single-linker loop), and the links compared."""
+    from oracle import ref
+    from zipkin_amd import _native as N
+    from zipkin_amd import synth
+    w = synth.C4.scaled(traces)
+    cols = synth.generate(w)
+    # traces holding a merge run candidate: two spans with one (id, shared)
+    sh = ((cols.port_flags >> np.uint32(19)) & np.uint32(3)) == 2
+    tix = np.repeat(np.arange(cols.n_traces), np.diff(cols.offsets.astype(np.int64)))
+    key = np.stack([tix, cols.id.view(np.int64), sh.astype(np.int64)])
+    o = np.lexsort(key[::-1])
+    dup = np.all(key[:, o][:, 1:] == key[:, o][:, :-1], axis=0)
+    merge_traces = int(np.unique(key[0, o][1:][dup]).size)
+    ctx = N.Context(w.total_services, device=device)
+    ts = []
+    out = None
+    for _ in range(reps + 1):
+        ctx.reset()
+        t0 = time.perf_counter()
+        synth.put_trace_loop(ctx, cols)
+        out = ctx.link()
+        ts.append(time.perf_counter() - t0)
+    ctx.close()
+    t = float(np.median(ts[1:]))
+    t1 = time.perf_counter()
+    st, op, oc, on, oe = ref.link(cols, threads=1)
+    t_one = time.perf_counter() - t1
+    same = st == 0 and _same_links(out, (op, oc, on, oe))
+    return {"workload": w.name, "traces": cols.n_traces, "spans": cols.n_spans, "merge_run_traces": merge_traces,
+            "ms": t * 1e3, "spans_per_s": cols.n_spans / t, "us_per_call": t / cols.n_traces * 1e6,
+            "cpu_single_thread_ms": t_one * 1e3, "cpu_single_thread_spans_per_s": cols.n_spans / t_one,
+            "speedup_vs_single_thread": t_one / t,
+            "parity": "bit-exact vs C++ restatement" if same else "MISMATCH",
+            "note": "one zdl_put_trace per trace from native code + zdl_link, host columns, PCIe-inclusive; "
+                    "the CPU figure is one linker on one thread over the same traces"}
+
+
 def _sorted_links(p, c, n, e):
     o = np.lexsort((c, p))
     return p[o], c[o], n[o], e[o]
@@ -578,7 +621,7 @@ def main():
     ap.add_argument("--timing-stride", type=int, default=8,
                     help="k_link HIP events around every n-th put of a context (roofline.achieved)")
     ap.add_argument("--inflight", type=int, default=0,
-                    help="steps in flight (contexts used round-robin): default 2 at N = 1, 1 at N > 1")
+                    help="steps in flight (contexts used round-robin): default 2")
     ap.add_argument("--no-insertion-order", action="store_true",
                     help="skip the side measurement of the insertion-order mode (N = 1 only)")
     args = ap.parse_args()
@@ -705,12 +748,20 @@ def main():
     kts = [x for x in kts if x > 0] or [float("nan")]
     tiles_inflight = float(np.mean(kts))
     shared_ms = None
-    if inflight > 1:  # the same in-flight steps with every context reading ONE copy of the batch
-        sync_all()
-        t1 = time.perf_counter()
-        run(args.steps, shared=True)
-        sync_all()
-        shared_ms = (time.perf_counter() - t1) / args.steps * 1e3
+    legs = None
+    if inflight > 1:
+        # the same in-flight steps with every context reading ONE copy of the batch, interleaved
+        # with more distinct-copy legs (shared, distinct, shared, distinct after the headline
+        # leg): a difference that follows the input and not the position is the input's
+        legs = []
+        for shared in (True, False, True, False):
+            sync_all()
+            t1 = time.perf_counter()
+            run(args.steps, shared=shared)
+            sync_all()
+            legs.append({"input": "shared" if shared else "distinct",
+                         "ms_per_step": (time.perf_counter() - t1) / args.steps * 1e3})
+        shared_ms = float(np.median([g["ms_per_step"] for g in legs if g["input"] == "shared"]))
     # The step's contexts are done: close them before the serial leg and the side legs. Each
     # context owns a HIP stream, and with GPU_MAX_HW_QUEUES=4 (the box's setting) streams beyond
     # four share hardware queues - the C5 leg's two contexts then ran one after the other (7.7 ms
@@ -815,6 +866,12 @@ def main():
         ptl = put_trace_leg(cols, S, local, (p, c, n, e))
         log(f"putTrace loop: {ptl['ms']:.1f} ms for {ptl['calls']} calls ({ptl['spans_per_s']:.3e} spans/s, "
             f"{ptl['us_per_call']:.3f} us/call), links {ptl['parity']}")
+    ptc4 = None
+    if side and not args.no_put_trace:
+        ptc4 = put_trace_c4_leg(local)
+        log(f"putTrace loop c4: {ptc4['ms']:.1f} ms for {ptc4['traces']} calls ({ptc4['merge_run_traces']} with merge "
+            f"runs), {ptc4['us_per_call']:.3f} us/call; one C++ linker on 1 thread {ptc4['cpu_single_thread_ms']:.0f} "
+            f"ms ({ptc4['speedup_vs_single_thread']:.1f}x), links {ptc4['parity']}")
     c5 = None
     if side and not args.no_c5:
         c5 = c5_leg(local, parity=not args.no_parity, threads=cpu_info()["usable"], host_threads=args.c5_host_threads)
@@ -885,6 +942,9 @@ def main():
                        "services": S, "parallelism": f"trace-shard x{world}", "combine": combine,
                        "inflight": inflight, "ms_per_step_serial": serial_ms,
                        "ms_per_step_shared_input": shared_ms,
+                       "interleaved_legs": legs,
+                       "step_roofline_frac_serial": (bytes_launch / (serial_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+                                                     if serial_ms else None),
                        "kernel_ms": {"k_link": tiles,
                                      "k_link_source": "HIP events around every k_link of the serial leg (one "
                                                       "step at a time, nothing else on the GPU)" if world == 1
@@ -894,7 +954,7 @@ def main():
                        "k_link_read_frac": read_launch / (tiles * 1e-3) / 1e9 / HBM_PEAK_GBS,
                        "parity": parity, "links": int(len(p)), "insertion_order": ins, "host_buffers": h2d,
                        "proto3_ingest": p3, "json_v2_ingest": jleg, "store_get_dependencies": sleg,
-                       "mysql_rows": rows_leg, "put_trace_loop": ptl, "c5": c5},
+                       "mysql_rows": rows_leg, "put_trace_loop": ptl, "put_trace_loop_c4": ptc4, "c5": c5},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "k_link", "algorithmic_bytes_per_launch": klink_bytes,

@@ -36,11 +36,12 @@
 extern "C" {
 #endif
 
-#define ZDL_ABI_VERSION 5  /* 2: zdl_config.n_devices / device_ids, RCCL combine; 3: zdl_kernel_times
+#define ZDL_ABI_VERSION 6  /* 2: zdl_config.n_devices / device_ids, RCCL combine; 3: zdl_kernel_times
                               per phase of a put (mid_ms, giant_ms, sparse_ms); 4: trace id widths
                               (zdl_store_append_ids, zdl_decoded.dev_trace_wide); 5: zdl_put_trace,
                               a trace whose Trace.merge throws adds nothing, a started link locks
-                              the context until zdl_link_finish */
+                              the context until zdl_link_finish; 6: zdl_comm_init_local (a job of
+                              contexts of one process), a sparse job sums by reduce-scatter */
 
 /* ---- status codes ---- */
 #define ZDL_OK          0
@@ -367,11 +368,22 @@ int zdl_table_import(zdl_ctx* ctx, const void* dev_call, const void* dev_err);
 /* ---- multi-process jobs (one process per GPU, e.g. torch.distributed.run): each process
  * makes a one-device context and joins one RCCL communicator; from then on zdl_link and
  * zdl_table_export of every rank sum the tables of all ranks (ncclAllReduce over xGMI) and
- * return the job's links. Rank 0 makes the id and sends its 128 bytes to the others. Not with
- * ZDL_FLAG_INSERTION_ORDER or daily buckets. ---- */
+ * return the job's links (ZDL_ORDER_INSERTION: DependencyLinker.merge over the ranks' lists in
+ * rank order). Rank 0 makes the id and sends its 128 bytes to the others. Not with daily
+ * buckets. ---- */
 #define ZDL_COMM_ID_BYTES 128
 int zdl_comm_unique_id(uint8_t* out /* ZDL_COMM_ID_BYTES */);
 int zdl_comm_init(zdl_ctx* ctx, const uint8_t* id, int rank, int world);
+
+/* A job of `world` contexts of THIS process (ctxs[k] becomes rank k), all on one device, with
+ * one service count and mode: the same combines as an RCCL job (zdl_link / zdl_table_export of
+ * every rank return the job's links, insertion order included), the transport being device
+ * copies and an element-wise reduce kernel instead of RCCL (zipkin_amd/csrc/zdl_xport.inc).
+ * Like the processes of an RCCL job, the ranks' zdl_link (or zdl_table_export) calls must run
+ * concurrently, one thread per context; a rank that never arrives makes the others fail after
+ * ZDL_LOCAL_WORLD_TIMEOUT_S seconds (default 120). For shards that share a GPU, and for testing
+ * a job's combines on one GPU. Destroying any rank's context ends the job for all. */
+int zdl_comm_init_local(zdl_ctx* const* ctxs, int world);
 
 /* Device-resident, already sharded input of a device group: cols[d] / n_spans[d] /
  * offsets[d] / n_traces[d] live on device_ids[d] (zdl_put_spans_device per device,

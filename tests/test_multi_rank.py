@@ -1,30 +1,32 @@
-"""Multi-process path on CPU (gloo, world_size 2): traces sharded by the low 64 bits
-of the trace id, each rank links its shard, one all-reduce of the S x S tables
-(zipkin_amd.shard.combine_tables, the same call bench.py makes over RCCL) equals
-linking everything at once. The per-rank linking uses the C++ restatement here
-(no GPU in this container); on the GPU box the engine fills the table."""
+"""The sharding the multi-GPU path relies on, checked on CPU with world-size-2 gloo processes.
+
+Traces shard by splitmix64 of the low 64 bits of the trace id (shard.partition_columns, the
+same rule as zdl_shard_of and bench.py's per-rank generator), so no trace crosses ranks, and
+the job's result is DependencyLinker.merge over the ranks' lists (DependencyLinker.java:189-204).
+Here each gloo rank runs the oracle over its own shard and the ranks exchange their lists
+(all_gather_object): the merged sums equal one linker over every trace. This checks the
+sharding rule and the merge semantics only - the oracle stands in for each rank's linker. The
+engine's own combines (libzdl: the sum / MIN all-reduces and the sparse reduce-scatter) run
+with W = 2, 3 and 8 ranks on one GPU in tests/test_gpu_local_world.py."""
 import os
 import socket
+from collections import namedtuple
 
 import numpy as np
-import pytest
-import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
+from oracle import dl_oracle as O
 from oracle import ref
 from zipkin_amd import shard, synth
 
+Link = namedtuple("Link", "parent child call_count error_count")
 
-def _table(cols, S):
+
+def _links(cols):
     st, p, c, n, e = ref.link(cols, threads=2)
     assert st == 0
-    call = torch.zeros(S * S, dtype=torch.int64)
-    err = torch.zeros(S * S, dtype=torch.int64)
-    idx = torch.from_numpy(p.astype(np.int64) * S + c)
-    call[idx] = torch.from_numpy(n)
-    err[idx] = torch.from_numpy(e)
-    return call, err
+    return list(zip(p.tolist(), c.tolist(), n.tolist(), e.tolist()))
 
 
 def _worker(rank, world, port, out):
@@ -33,10 +35,13 @@ def _worker(rank, world, port, out):
     w = synth.C4.scaled(4000)
     cols = synth.generate(w, threads=2)
     mine = shard.partition_columns(cols, world)[rank]
-    call, err = _table(mine, w.total_services)
-    shard.combine_tables(call, err)
+    # every trace of this rank's shard hashes to this rank (no trace crosses ranks)
+    lo = mine.trace_lo[mine.offsets[:-1].astype(np.int64)] if mine.n_traces else np.zeros(0, np.uint64)
+    assert (shard.shard_of(lo, world) == rank).all()
+    lists = [None] * world
+    dist.all_gather_object(lists, _links(mine) if mine.n_spans else [])
     if rank == 0:
-        out.put((call.numpy().copy(), err.numpy().copy()))
+        out.put(lists)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -49,23 +54,24 @@ def _free_port():
     return p
 
 
-def test_two_rank_shard_and_combine_equals_single():
+def test_two_rank_shards_merge_to_the_whole():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, 2, PORT, q)) for r in range(2)]
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    call, err = q.get(timeout=120)
+    lists = q.get(timeout=120)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     w = synth.C4.scaled(4000)
     full = synth.generate(w, threads=2)
-    c1, e1 = _table(full, w.total_services)
-    assert np.array_equal(call, c1.numpy()) and np.array_equal(err, e1.numpy())
-
-
-PORT = _free_port()
+    # the oracle's merge keys links by service name: ids as names, and back
+    merged = O.DependencyLinker.merge([Link(f"s{a}", f"s{b}", n, e) for lst in lists for a, b, n, e in lst])
+    got = sorted((int(l.parent[1:]), int(l.child[1:]), l.call_count, l.error_count) for l in merged)
+    assert got == sorted(_links(full))
+    assert sum(len(lst) for lst in lists) > len(got)  # both ranks saw some of the same pairs
 
 
 def test_partition_keeps_mixed_width_trace_ids_together():

@@ -90,6 +90,95 @@ static void check_sparse(std::mt19937_64& r, int W, bool all) {
   }
 }
 
+// A job's sparse reduce-scatter (comm_sum_sparse): each rank samples its sorted list, every rank
+// derives the same range bounds (range_split), cuts its list into W slices by lower bound, the
+// W x W slice lengths give every rank its slice_plan; the plans' sends and receives agree, the
+// slices land where the receivers expect them, each rank's received runs summed per cell lie in
+// its range, and the reduced ranges concatenated in rank order are the job's list: sorted, each
+// cell once, with the summed counts.
+static void check_reduce_scatter(std::mt19937_64& r, int W) {
+  const uint32_t q = SPLIT_SAMPLES;
+  const uint32_t span = 1 + (uint32_t)(r() % 3 == 0 ? 3 : (r() % 2 ? 500 : 4000000000u));
+  std::vector<std::vector<Entry>> lists(W);
+  for (int k = 0; k < W; ++k) {
+    const int len = (r() % 4 == 0) ? 0 : (int)(r() % 300);
+    std::map<uint32_t, Entry> m;
+    for (int i = 0; i < len; ++i) {
+      // skewed cells (a Zipf-like head), some shared by every rank
+      const uint32_t cell = (r() % 3 == 0) ? (uint32_t)(r() % 4) : (uint32_t)(r() % span);
+      auto& e = m[cell];
+      e.cell = cell;
+      e.call += 1 + r() % 5;
+      e.err += r() % 2;
+    }
+    for (auto& kv : m) lists[k].push_back(kv.second);
+  }
+  std::vector<uint64_t> meta((size_t)W * (1 + q));
+  for (int k = 0; k < W; ++k) {
+    const uint64_t n = lists[k].size();
+    meta[(size_t)k * (1 + q)] = n;
+    for (uint32_t i = 0; i < q; ++i)  // k_x_samples
+      meta[(size_t)k * (1 + q) + 1 + i] = n ? lists[k][((2 * (uint64_t)i + 1) * n) / (2 * (uint64_t)q)].cell : 0;
+  }
+  const std::vector<uint64_t> b = range_split(meta.data(), W, q);
+  CHECK((int)b.size() == W + 1 && b[0] == 0 && b[W] == (1ull << 32));
+  for (int k = 0; k < W; ++k) CHECK(b[k] <= b[k + 1]);
+  std::vector<uint64_t> cnt((size_t)W * W);
+  for (int k = 0; k < W; ++k)  // k_x_slices
+    for (int j = 0; j < W; ++j) {
+      auto lb = [&](uint64_t v) {
+        return (uint64_t)(std::lower_bound(lists[k].begin(), lists[k].end(), v,
+                                           [](const Entry& e, uint64_t x) { return (uint64_t)e.cell < x; }) -
+                          lists[k].begin());
+      };
+      cnt[(size_t)k * W + j] = lb(b[j + 1]) - lb(b[j]);
+    }
+  std::vector<Plan> plans;
+  for (int me = 0; me < W; ++me) plans.push_back(slice_plan(cnt.data(), W, me));
+  std::vector<std::vector<Entry>> buf(W);
+  for (int me = 0; me < W; ++me) buf[me].assign(plans[me].total(), Entry{~0u, 0, 0});
+  for (int me = 0; me < W; ++me)
+    for (const Xfer& x : plans[me].ops) {
+      CHECK(x.n > 0 && (x.src == me || x.dst == me));
+      if (x.src != me) {  // a receive: the sender's plan holds the same transfer
+        bool found = false;
+        for (const Xfer& y : plans[x.src].ops)
+          if (y.src == x.src && y.dst == me) {
+            CHECK(!found && y.n == x.n && y.at == x.at && y.from == x.from);
+            found = true;
+          }
+        CHECK(found);
+        continue;
+      }
+      CHECK(x.from + x.n <= lists[me].size() && x.at + x.n <= buf[x.dst].size());
+      std::copy(lists[me].begin() + x.from, lists[me].begin() + x.from + x.n, buf[x.dst].begin() + x.at);
+    }
+  std::map<uint32_t, std::pair<uint64_t, uint64_t>> want;
+  for (auto& l : lists)
+    for (auto& e : l) {
+      want[e.cell].first += e.call;
+      want[e.cell].second += e.err;
+    }
+  std::vector<Entry> job;
+  for (int me = 0; me < W; ++me) {
+    std::map<uint32_t, Entry> red;  // sparse_add
+    for (auto& e : buf[me]) {
+      CHECK(e.cell != ~0u && e.cell >= b[me] && e.cell < b[me + 1]);
+      auto& x = red[e.cell];
+      x.cell = e.cell;
+      x.call += e.call;
+      x.err += e.err;
+    }
+    for (auto& kv : red) job.push_back(kv.second);
+  }
+  CHECK(job.size() == want.size());
+  size_t i = 0;
+  for (auto& kv : want) {
+    CHECK(job[i].cell == kv.first && job[i].call == kv.second.first && job[i].err == kv.second.second);
+    ++i;
+  }
+}
+
 // Insertion order: each rank's first-seen ranks tagged by ord_tag, the element-wise MIN over
 // the ranks, then sorting the non-empty cells by it gives DependencyLinker.merge's order over
 // the ranks' link() lists concatenated in rank order.
@@ -135,7 +224,9 @@ int main() {
     check_sparse(r, W, true);
     check_sparse(r, W, false);
     check_ord(r, W);
+    check_reduce_scatter(r, W);
   }
+  for (int W : {16, 64}) check_reduce_scatter(r, W);
   check_ord(r, ORD_MAX_WORLD);
   std::printf("ok\n");
   return 0;

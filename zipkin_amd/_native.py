@@ -49,9 +49,9 @@ EXPORTS = (
     "zdl_decoder_download", "zdl_decoder_kernel_ms", "zdl_put_mysql_rows", "zdl_rows_last_error",
     "zdl_comm_unique_id", "zdl_comm_init", "zdl_put_spans_device_multi", "zdl_device_count", "zdl_shard_of",
     "zdl_tree_export", "zdl_tree_reasons", "zdl_decode_json_v2", "zdl_decode_retry", "zdl_decoder_struct_ms", "zdl_decoder_exact_spans",
-    "zdl_link_start", "zdl_link_finish", "zdl_put_trace",
+    "zdl_link_start", "zdl_link_finish", "zdl_put_trace", "zdl_comm_init_local",
 )
-ZDL_ABI_VERSION = 5
+ZDL_ABI_VERSION = 6
 ZDL_COMM_ID_BYTES = 128
 
 
@@ -212,6 +212,8 @@ def lib() -> C.CDLL:
     L.zdl_comm_unique_id.restype = C.c_int
     L.zdl_comm_init.argtypes = [vp, vp, C.c_int, C.c_int]
     L.zdl_comm_init.restype = C.c_int
+    L.zdl_comm_init_local.argtypes = [vp, C.c_int]
+    L.zdl_comm_init_local.restype = C.c_int
     L.zdl_put_spans_device_multi.argtypes = [vp, C.POINTER(SpanCols), vp, vp, vp]
     L.zdl_put_spans_device_multi.restype = C.c_int
     L.zdl_device_count.argtypes = [vp]
@@ -301,6 +303,16 @@ class Context:
         """Joins a multi-process job (zdl_comm_init): link() then returns every rank's links."""
         b = C.create_string_buffer(bytes(uid), ZDL_COMM_ID_BYTES)
         self.check(self._L.zdl_comm_init(self.h, b, int(rank), int(world)))
+
+    @staticmethod
+    def comm_init_local(ctxs) -> None:
+        """zdl_comm_init_local: contexts of this process (one device) become ranks 0..W-1 of one
+        job; each rank's link() must then run on its own thread, concurrently with the others'."""
+        hs = (C.c_void_p * len(ctxs))(*[c.h.value for c in ctxs])
+        rc = lib().zdl_comm_init_local(hs, len(ctxs))
+        if rc != ZDL_OK:
+            msg = next((c._L.zdl_last_error(c.h).decode() for c in ctxs if c._L.zdl_last_error(c.h)), "")
+            raise ZdlError(rc, msg or "zdl_comm_init_local failed")
 
     @staticmethod
     def comm_unique_id() -> bytes:

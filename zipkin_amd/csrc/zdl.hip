@@ -1622,7 +1622,10 @@ struct zdl_ctx {
   std::vector<zdl_ctx*> sub;
   std::vector<ncclComm_t> comms;
   ncclComm_t comm = nullptr;
+  struct LocalWorld* lworld = nullptr;  // zdl_comm_init_local: ranks are contexts of this process (zdl_xport.inc)
   int comm_rank = 0, comm_world = 1;
+  DevBuf<unsigned long long> xs[3];  // the local transport's reduce scratch
+  SparseTable gslice;                // sparse combine: this rank's cell range of the job's list
   DevBuf<unsigned long long> red_call, red_err;  // the summed tables
   DevBuf<unsigned long long> red_first;          // insertion order: the job's first ranks (MIN)
   // sparse combine (device groups / jobs above 1024 services): every device's or rank's sorted
@@ -1727,6 +1730,10 @@ struct zdl_ctx {
   bool link_async = false;  // the started link is a sparse compaction in flight
   Stage stg;                // zdl_put_trace's staged traces
 };
+
+// a rank of a job: RCCL (zdl_comm_init) or a local world (zdl_comm_init_local)
+static inline bool in_job(const zdl_ctx* c) { return c->comm != nullptr || c->lworld != nullptr; }
+static void lw_release(zdl_ctx* c);  // zdl_xport.inc
 
 namespace {
 
@@ -1984,6 +1991,7 @@ void zdl_destroy(zdl_ctx* c) {
     return;
   }
   if (c->comm) (void)ncclCommDestroy(c->comm);
+  lw_release(c);
   (void)hipSetDevice(c->device);
   (void)resolve_lazy(c, false);
   stage_free(c);
@@ -1993,6 +2001,8 @@ void zdl_destroy(zdl_ctx* c) {
   c->red_call.release();
   c->red_err.release();
   c->red_first.release();
+  for (auto& x : c->xs) x.release();
+  c->gslice.release();
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (auto& r : c->rank) r.release();
@@ -2108,7 +2118,7 @@ int zdl_set_days(zdl_ctx* c, int64_t day0_ms, uint32_t n_days) {
   if (!c) return ZDL_EINVAL;
   if (c->link_pending >= 0) return fail(c, ZDL_EINVAL, "zdl_set_days: a started link is not finished (zdl_link_finish)");
   if (const int frc = stage_flush(c)) return frc;  // staged putTrace calls come first
-  if (!c->sub.empty() || c->comm) return fail(c, ZDL_EINVAL, "zdl_set_days: one device, one process");
+  if (!c->sub.empty() || in_job(c)) return fail(c, ZDL_EINVAL, "zdl_set_days: one device, one process");
   if (c->sparse) return fail(c, ZDL_EINVAL, "zdl_set_days: needs the S x S table (a sparse context has none)");
   if (n_days > 255) return fail(c, ZDL_EINVAL, "zdl_set_days: at most 255 days");
   if (n_days && (day0_ms % DAY_MS) != 0) return fail(c, ZDL_EINVAL, "zdl_set_days: day0 must be a UTC midnight");
@@ -3769,7 +3779,7 @@ int zdl_link(zdl_ctx* c, int order, zdl_links* out) {
   if (order == ZDL_ORDER_INSERTION) {
     if (!c->ord) return fail(c, ZDL_EINVAL, "ZDL_ORDER_INSERTION needs a ZDL_FLAG_INSERTION_ORDER context");
     HIP_TRY(c, enter(c));
-    if (c->comm) {  // a rank of a job: DependencyLinker.merge over the ranks' lists in rank order
+    if (in_job(c)) {  // a rank of a job: DependencyLinker.merge over the ranks' lists in rank order
       const int rc = comm_sum_ord(c);
       if (rc != ZDL_OK) return rc;
       return link_insertion(c, out, c->red_call.p, c->red_err.p, c->red_first.p);
@@ -3778,13 +3788,13 @@ int zdl_link(zdl_ctx* c, int order, zdl_links* out) {
   }
   if (order != ZDL_ORDER_SORTED) return fail(c, ZDL_EINVAL, "zdl_link: order must be ZDL_ORDER_SORTED or ZDL_ORDER_INSERTION");
   HIP_TRY(c, enter(c));
-  if (c->sparse && c->comm) {  // a rank of a multi-process job: every rank's list, summed
+  if (c->sparse && in_job(c)) {  // a rank of a job: every rank's list, summed
     const int rc = comm_sum_sparse(c);
     if (rc != ZDL_OK) return rc;
     return link_sparse(c, out, &c->gacc);
   }
   if (c->sparse) return link_sparse(c, out);
-  if (c->comm) {  // a rank of a multi-process job: the links of every rank's tables
+  if (in_job(c)) {  // a rank of a job: the links of every rank's tables
     const int rc = comm_sum_tables(c);
     if (rc != ZDL_OK) return rc;
     return link_sorted(c, c->red_call.p, c->red_err.p, false, out);
@@ -3798,7 +3808,7 @@ int zdl_link_start(zdl_ctx* c, int order) {
   if (const int frc = stage_flush(c)) return frc;
   c->link_pending = order;
   c->link_async = false;
-  if (c->sparse && !c->comm && c->sub.empty() && order == ZDL_ORDER_SORTED && !c->poisoned) {
+  if (c->sparse && !in_job(c) && c->sub.empty() && order == ZDL_ORDER_SORTED && !c->poisoned) {
     HIP_TRY(c, enter(c));
     int rc = link_sparse_start(c, c->acc);
     if (rc == ZDL_OK) rc = rec_launch(c);  // the records cross PCIe on an SDMA engine meanwhile
@@ -3831,7 +3841,7 @@ int zdl_link_days(zdl_ctx* c, int order, zdl_day_links* out) {
   if (!c || !out) return ZDL_EINVAL;
   if (c->link_pending >= 0) return fail(c, ZDL_EINVAL, "zdl_link_days: a started link is not finished (zdl_link_finish)");
   if (const int frc = stage_flush(c)) return frc;  // staged putTrace calls come first
-  if (!c->sub.empty() || c->comm) return fail(c, ZDL_EINVAL, "zdl_link_days: one device, one process");
+  if (!c->sub.empty() || in_job(c)) return fail(c, ZDL_EINVAL, "zdl_link_days: one device, one process");
   if (!c->days) return fail(c, ZDL_EINVAL, "zdl_link_days: no daily buckets (zdl_set_days)");
   if (order == ZDL_ORDER_INSERTION && !c->ord)
     return fail(c, ZDL_EINVAL, "ZDL_ORDER_INSERTION needs a ZDL_FLAG_INSERTION_ORDER context");
@@ -4073,7 +4083,7 @@ int zdl_table_export(zdl_ctx* c, void* dev_call, void* dev_err) {
     const int lrc = resolve_lazy(c, false);  // a lazy put's k_mid / k_tail before the table is used
     if (lrc != ZDL_OK) return lrc;
   }
-  if (c->comm) {  // every rank's tables, summed
+  if (in_job(c)) {  // every rank's tables, summed
     const int rc = comm_sum_tables(c);
     if (rc != ZDL_OK) return rc;
     const size_t bytes = (size_t)c->rows * c->S * 8;
@@ -4362,17 +4372,15 @@ int group_export(zdl_ctx* g, void* dev_call, void* dev_err) {
   return group_reduce(g, (unsigned long long*)dev_call, (unsigned long long*)dev_err);
 }
 
+#include "zdl_xport.inc"  // the transport under the combines: RCCL or a local world
+
+// Every rank's tables, summed (DependencyLinker.merge over the ranks' maps, DependencyLinker.java:189-204)
 static int comm_sum_tables(zdl_ctx* c) {
   const size_t SS = (size_t)c->rows * c->S;
   HIP_TRY(c, c->red_call.ensure(SS));
   HIP_TRY(c, c->red_err.ensure(SS));
-  ncclResult_t r = ncclGroupStart();
-  if (r == ncclSuccess) r = ncclAllReduce(c->call.p, c->red_call.p, SS, ncclUint64, ncclSum, c->comm, c->stream);
-  if (r == ncclSuccess) r = ncclAllReduce(c->errc.p, c->red_err.p, SS, ncclUint64, ncclSum, c->comm, c->stream);
-  const ncclResult_t r2 = ncclGroupEnd();
-  if (r != ncclSuccess || r2 != ncclSuccess)
-    return fail(c, ZDL_EDEVICE, std::string("ncclAllReduce: ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
-  return ZDL_OK;
+  const XRed ops[2] = {{c->call.p, c->red_call.p, SS, 0}, {c->errc.p, c->red_err.p, SS, 0}};
+  return x_allreduce(c, ops, 2);
 }
 
 // Each rank's first-seen ranks tagged with the job rank above them (zdl_xplan::ord_tag)
@@ -4382,9 +4390,9 @@ __global__ void k_ord_tag(const unsigned long long* __restrict__ first, unsigned
     out[i] = zdl_xplan::ord_tag(first[i], rank);
 }
 
-// Insertion order across a job (zdl_xplan.h): the sums as comm_sum_tables, and one ncclMin of
-// the rank-tagged first ranks, so a pair sits where DependencyLinker.merge over the ranks'
-// link() lists, concatenated in rank order, first sees it (DependencyLinker.java:189-204).
+// Insertion order across a job (zdl_xplan.h): the sums as comm_sum_tables, and one MIN of the
+// rank-tagged first ranks, so a pair sits where DependencyLinker.merge over the ranks' link()
+// lists, concatenated in rank order, first sees it (DependencyLinker.java:189-204).
 static int comm_sum_ord(zdl_ctx* c) {
   if (c->span_base >= zdl_xplan::ORD_POS_LIMIT)
     return fail(c, ZDL_EINVAL, "insertion order across ranks: more than 2^34 spans put on this rank");
@@ -4395,61 +4403,133 @@ static int comm_sum_ord(zdl_ctx* c) {
   hipLaunchKernelGGL(k_ord_tag, dim3((unsigned)std::min<size_t>((SS + 255) / 256, 4096)), dim3(256), 0, c->stream,
                      c->first.p, c->red_first.p, (uint64_t)SS, c->comm_rank);
   HIP_TRY(c, hipGetLastError());
-  ncclResult_t r = ncclGroupStart();
-  if (r == ncclSuccess) r = ncclAllReduce(c->call.p, c->red_call.p, SS, ncclUint64, ncclSum, c->comm, c->stream);
-  if (r == ncclSuccess) r = ncclAllReduce(c->errc.p, c->red_err.p, SS, ncclUint64, ncclSum, c->comm, c->stream);
-  if (r == ncclSuccess)
-    r = ncclAllReduce(c->red_first.p, c->red_first.p, SS, ncclUint64, ncclMin, c->comm, c->stream);
-  const ncclResult_t r2 = ncclGroupEnd();
-  if (r != ncclSuccess || r2 != ncclSuccess)
-    return fail(c, ZDL_EDEVICE, std::string("ncclAllReduce: ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
-  return ZDL_OK;
+  const XRed ops[3] = {{c->call.p, c->red_call.p, SS, 0}, {c->errc.p, c->red_err.p, SS, 0},
+                       {c->red_first.p, c->red_first.p, SS, 1}};
+  return x_allreduce(c, ops, 3);
 }
 
-// Multi-process jobs above 1024 services: the ranks' list lengths by ncclAllGather, then every
-// rank's list to every rank (ncclSend / ncclRecv, exact lengths: an all-gather of unequal
-// parts), summed per cell on each rank (sparse_add) - every rank returns the job's links.
+// The sampled cells of a rank's sorted list: meta[0] = n, meta[1 + i] = cell at the middle of the
+// i-th of q equal parts (zdl_xplan::range_split)
+__global__ void k_x_samples(const uint32_t* __restrict__ cell, uint64_t n, uint32_t q, uint64_t* __restrict__ meta) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) meta[0] = n;
+  if (i < q) meta[1 + i] = n ? cell[((2 * (uint64_t)i + 1) * n) / (2 * (uint64_t)q)] : 0;
+}
+
+// cnt[k] = entries of the sorted list in [split[k], split[k + 1]) (lower bounds; split[W] = 2^32)
+__global__ void k_x_slices(const uint32_t* __restrict__ cell, uint64_t n, const uint64_t* __restrict__ split, int W,
+                           uint64_t* __restrict__ cnt) {
+  __shared__ uint64_t lb[zdl_xplan::MAX_WORLD + 1];
+  for (int k = threadIdx.x; k <= W; k += blockDim.x) {
+    const uint64_t v = split[k];
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if ((uint64_t)cell[mid] < v) lo = mid + 1; else hi = mid;
+    }
+    lb[k] = lo;
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < W; k += blockDim.x) cnt[k] = lb[k + 1] - lb[k];
+}
+
+// Multi-rank jobs above 1024 services: a reduce-scatter by cell range,
+// then an all-gather of the reduced ranges. Every rank's list is sorted by cell, so
+//  1. each rank samples its list (q cells, and its length), one all-gather of the samples, and
+//     every rank picks the same W - 1 splitters from them (zdl_xplan::range_split);
+//  2. each rank's list falls into W contiguous slices, slice k to rank k: one all-gather of the
+//     W x W slice lengths, then every slice to its rank (point to point, exact lengths);
+//  3. each rank sums the W runs it received per cell (sparse_add: DependencyLinker.merge's sum)
+//     - only its cell range, about 1/W of all entries;
+//  4. one all-gather of the reduced ranges' lengths, then every range to every rank: ranges are
+//     disjoint and ascending with the rank, so the rank-order concatenation is the job's list,
+//     sorted, each cell once - no second sort.
+// Per rank that moves ~(own list + job list) entries and sorts ~1/W of the job's entries, where
+// gathering every list to every rank moved and sorted W lists (DESIGN §6 prices both at C5).
 static int comm_sum_sparse(zdl_ctx* c) {
   const int W = c->comm_world, me = c->comm_rank;
-  hipStream_t st = c->stream;
-  HIP_TRY(c, c->gx_n.ensure((size_t)W + 1));
-  HIP_TRY(c, hipMemcpyAsync(c->gx_n.p + W, &c->acc.n, 8, hipMemcpyHostToDevice, st));
-  ncclResult_t r = ncclAllGather(c->gx_n.p + W, c->gx_n.p, 1, ncclUint64, c->comm, st);
-  if (r != ncclSuccess) return fail(c, ZDL_EDEVICE, std::string("ncclAllGather: ") + ncclGetErrorString(r));
-  std::vector<uint64_t> n((size_t)W);
-  HIP_TRY(c, hipMemcpyAsync(n.data(), c->gx_n.p, 8 * (size_t)W, hipMemcpyDeviceToHost, st));
+  const hipStream_t st = c->stream;
+  const uint32_t q = zdl_xplan::SPLIT_SAMPLES;
+  const size_t mrow = 1 + (size_t)q;                 // one rank's sample block (u64)
+  const size_t mw = (size_t)W * mrow;                // the gathered samples
+  const size_t sw_off = 2 * mw, cnt_off = sw_off + (size_t)W + 1, cntg_off = cnt_off + (size_t)W;
+  HIP_TRY(c, c->gx_n.ensure(cntg_off + (size_t)W * W + 2 * (size_t)W));
+  uint64_t* meta = c->gx_n.p;
+  // 1. samples -> splitters
+  hipLaunchKernelGGL(k_x_samples, dim3((q + 255) / 256), dim3(256), 0, st, (const uint32_t*)c->acc.cell,
+                     (uint64_t)c->acc.n, q, meta + mw);
+  HIP_TRY(c, hipGetLastError());
+  if (const int rc = x_allgather(c, meta + mw, meta, mrow * 8)) return rc;
+  std::vector<uint64_t> hm(mw);
+  HIP_TRY(c, hipMemcpyAsync(hm.data(), meta, mw * 8, hipMemcpyDeviceToHost, st));
   HIP_TRY(c, hipStreamSynchronize(st));
-  const zdl_xplan::Plan plan = zdl_xplan::gather_plan(n.data(), W, true);  // every list to every rank
-  const uint64_t total = plan.total();
-  HIP_TRY(c, c->gx_cell.ensure(total));
-  HIP_TRY(c, c->gx_call.ensure(total));
-  HIP_TRY(c, c->gx_err.ensure(total));
-  r = ncclGroupStart();
-  for (const zdl_xplan::Xfer& x : plan.ops) {
-    if (x.src == x.dst || r != ncclSuccess) continue;
-    if (x.src == me) {
-      r = ncclSend(c->acc.cell, x.n, ncclUint32, x.dst, c->comm, st);
-      if (r == ncclSuccess) r = ncclSend(c->acc.call, x.n, ncclUint64, x.dst, c->comm, st);
-      if (r == ncclSuccess) r = ncclSend(c->acc.err, x.n, ncclUint64, x.dst, c->comm, st);
-    } else if (x.dst == me) {
-      r = ncclRecv(c->gx_cell.p + x.at, x.n, ncclUint32, x.src, c->comm, st);
-      if (r == ncclSuccess) r = ncclRecv(c->gx_call.p + x.at, x.n, ncclUint64, x.src, c->comm, st);
-      if (r == ncclSuccess) r = ncclRecv(c->gx_err.p + x.at, x.n, ncclUint64, x.src, c->comm, st);
+  const std::vector<uint64_t> split = zdl_xplan::range_split(hm.data(), W, q);
+  HIP_TRY(c, hipMemcpyAsync(meta + sw_off, split.data(), ((size_t)W + 1) * 8, hipMemcpyHostToDevice, st));
+  // 2. slice lengths, the W x W matrix, the all-to-all of the slices
+  hipLaunchKernelGGL(k_x_slices, dim3(1), dim3(64), 0, st, (const uint32_t*)c->acc.cell, (uint64_t)c->acc.n,
+                     (const uint64_t*)(meta + sw_off), W, meta + cnt_off);
+  HIP_TRY(c, hipGetLastError());
+  if (const int rc = x_allgather(c, meta + cnt_off, meta + cntg_off, (size_t)W * 8)) return rc;
+  std::vector<uint64_t> cnt((size_t)W * W);
+  HIP_TRY(c, hipMemcpyAsync(cnt.data(), meta + cntg_off, cnt.size() * 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(c, hipStreamSynchronize(st));
+  const zdl_xplan::Plan a2a = zdl_xplan::slice_plan(cnt.data(), W, me);
+  const uint64_t rtot = a2a.total();
+  HIP_TRY(c, c->gx_cell.ensure(std::max<uint64_t>(rtot, 1)));
+  HIP_TRY(c, c->gx_call.ensure(std::max<uint64_t>(rtot, 1)));
+  HIP_TRY(c, c->gx_err.ensure(std::max<uint64_t>(rtot, 1)));
+  std::vector<XSend> sends;
+  std::vector<XRecv> recvs;
+  for (const zdl_xplan::Xfer& x : a2a.ops) {
+    if (x.src == me && x.dst == me) {  // my own slice: a device copy
+      HIP_TRY(c, hipMemcpyAsync(c->gx_cell.p + x.at, c->acc.cell + x.from, x.n * 4, hipMemcpyDeviceToDevice, st));
+      HIP_TRY(c, hipMemcpyAsync(c->gx_call.p + x.at, c->acc.call + x.from, x.n * 8, hipMemcpyDeviceToDevice, st));
+      HIP_TRY(c, hipMemcpyAsync(c->gx_err.p + x.at, c->acc.err + x.from, x.n * 8, hipMemcpyDeviceToDevice, st));
+    } else if (x.src == me) {
+      sends.push_back({x.dst, c->acc.cell + x.from, x.n * 4});
+      sends.push_back({x.dst, c->acc.call + x.from, x.n * 8});
+      sends.push_back({x.dst, c->acc.err + x.from, x.n * 8});
+    } else {
+      recvs.push_back({x.src, c->gx_cell.p + x.at, x.n * 4});
+      recvs.push_back({x.src, c->gx_call.p + x.at, x.n * 8});
+      recvs.push_back({x.src, c->gx_err.p + x.at, x.n * 8});
     }
   }
-  const ncclResult_t r2 = ncclGroupEnd();
-  if (r != ncclSuccess || r2 != ncclSuccess)
-    return fail(c, ZDL_EDEVICE, std::string("ncclSend/Recv: ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
-  for (const zdl_xplan::Xfer& x : plan.ops) {
-    if (x.src != me || x.dst != me) continue;
-    HIP_TRY(c, hipMemcpyAsync(c->gx_cell.p + x.at, c->acc.cell, x.n * 4, hipMemcpyDeviceToDevice, st));
-    HIP_TRY(c, hipMemcpyAsync(c->gx_call.p + x.at, c->acc.call, x.n * 8, hipMemcpyDeviceToDevice, st));
-    HIP_TRY(c, hipMemcpyAsync(c->gx_err.p + x.at, c->acc.err, x.n * 8, hipMemcpyDeviceToDevice, st));
-  }
-  c->gacc.n = 0;
+  if (const int rc = x_exchange(c, sends, recvs)) return rc;
+  // 3. this rank's range, summed per cell
+  c->gslice.n = 0;
   int kb = 1;
   while ((1ull << kb) < (uint64_t)c->S * c->S) ++kb;
-  HIP_TRY(c, sparse_add(c->sw, c->gacc, c->gx_cell.p, c->gx_call.p, c->gx_err.p, total, kb, st));
+  HIP_TRY(c, sparse_add(c->sw, c->gslice, c->gx_cell.p, c->gx_call.p, c->gx_err.p, rtot, kb, st));
+  // 4. every reduced range to every rank, in rank order
+  uint64_t* rn = meta + cntg_off + (size_t)W * W;
+  HIP_TRY(c, hipMemcpyAsync(rn + W, &c->gslice.n, 8, hipMemcpyHostToDevice, st));
+  if (const int rc = x_allgather(c, rn + W, rn, 8)) return rc;
+  std::vector<uint64_t> n((size_t)W);
+  HIP_TRY(c, hipMemcpyAsync(n.data(), rn, 8 * (size_t)W, hipMemcpyDeviceToHost, st));
+  HIP_TRY(c, hipStreamSynchronize(st));
+  const zdl_xplan::Plan plan = zdl_xplan::gather_plan(n.data(), W, true);  // every range to every rank
+  const uint64_t total = plan.total();
+  HIP_TRY(c, sparse_reserve(c->gacc, total));
+  sends.clear();
+  recvs.clear();
+  for (const zdl_xplan::Xfer& x : plan.ops) {
+    if (x.src == me && x.dst == me) {
+      HIP_TRY(c, hipMemcpyAsync(c->gacc.cell + x.at, c->gslice.cell, x.n * 4, hipMemcpyDeviceToDevice, st));
+      HIP_TRY(c, hipMemcpyAsync(c->gacc.call + x.at, c->gslice.call, x.n * 8, hipMemcpyDeviceToDevice, st));
+      HIP_TRY(c, hipMemcpyAsync(c->gacc.err + x.at, c->gslice.err, x.n * 8, hipMemcpyDeviceToDevice, st));
+    } else if (x.src == me) {
+      sends.push_back({x.dst, c->gslice.cell, x.n * 4});
+      sends.push_back({x.dst, c->gslice.call, x.n * 8});
+      sends.push_back({x.dst, c->gslice.err, x.n * 8});
+    } else if (x.dst == me) {
+      recvs.push_back({x.src, c->gacc.cell + x.at, x.n * 4});
+      recvs.push_back({x.src, c->gacc.call + x.at, x.n * 8});
+      recvs.push_back({x.src, c->gacc.err + x.at, x.n * 8});
+    }
+  }
+  if (const int rc = x_exchange(c, sends, recvs)) return rc;
+  c->gacc.n = total;
   return ZDL_OK;
 }
 
@@ -4471,7 +4551,8 @@ int zdl_comm_init(zdl_ctx* c, const uint8_t* id, int rank, int world) {
   if (c->days) return fail(c, ZDL_EINVAL, "zdl_comm_init: daily buckets are per process");
   if (c->ord && world > zdl_xplan::ORD_MAX_WORLD)
     return fail(c, ZDL_EINVAL, "zdl_comm_init: insertion order across at most 64 ranks");
-  if (c->comm) return fail(c, ZDL_EINVAL, "zdl_comm_init: already joined");
+  if (in_job(c)) return fail(c, ZDL_EINVAL, "zdl_comm_init: already joined");
+  if (c->sparse && world > zdl_xplan::MAX_WORLD) return fail(c, ZDL_EINVAL, "zdl_comm_init: a sparse job has at most 1024 ranks");
   HIP_TRY(c, enter(c));
   ncclUniqueId u;
   memcpy(&u, id, sizeof u);
@@ -4482,6 +4563,41 @@ int zdl_comm_init(zdl_ctx* c, const uint8_t* id, int rank, int world) {
   }
   c->comm_rank = rank;
   c->comm_world = world;
+  return ZDL_OK;
+}
+
+int zdl_comm_init_local(zdl_ctx* const* ctxs, int world) {
+  if (!ctxs || world < 1 || world > zdl_xplan::MAX_WORLD) return ZDL_EINVAL;
+  for (int k = 0; k < world; ++k) {
+    zdl_ctx* c = ctxs[k];
+    if (!c) return ZDL_EINVAL;
+    for (int j = 0; j < k; ++j)
+      if (ctxs[j] == c) return fail(c, ZDL_EINVAL, "zdl_comm_init_local: a context listed twice");
+    if (c->link_pending >= 0) return fail(c, ZDL_EINVAL, "zdl_comm_init_local: a started link is not finished (zdl_link_finish)");
+    if (const int frc = stage_flush(c)) return frc;  // staged putTrace calls come first
+    if (!c->sub.empty()) return fail(c, ZDL_EINVAL, "zdl_comm_init_local: a device group has its own communicator");
+    if (c->days) return fail(c, ZDL_EINVAL, "zdl_comm_init_local: daily buckets are per process");
+    if (in_job(c)) return fail(c, ZDL_EINVAL, "zdl_comm_init_local: already joined");
+    if (c->ord && world > zdl_xplan::ORD_MAX_WORLD)
+      return fail(c, ZDL_EINVAL, "zdl_comm_init_local: insertion order across at most 64 ranks");
+    const zdl_ctx* c0 = ctxs[0];
+    if (c->device != c0->device || c->S != c0->S || c->rows != c0->rows || c->sparse != c0->sparse || c->ord != c0->ord)
+      return fail(c, ZDL_EINVAL, "zdl_comm_init_local: the ranks need one device, one service count and one mode");
+  }
+  LocalWorld* w = new LocalWorld;
+  w->W = world;
+  w->device = ctxs[0]->device;
+  w->refs = world;
+  w->board.resize((size_t)world);
+  if (const char* e = getenv("ZDL_LOCAL_WORLD_TIMEOUT_S")) {
+    const double t = atof(e);
+    if (t > 0) w->timeout_s = t;
+  }
+  for (int k = 0; k < world; ++k) {
+    ctxs[k]->lworld = w;
+    ctxs[k]->comm_rank = k;
+    ctxs[k]->comm_world = world;
+  }
   return ZDL_OK;
 }
 

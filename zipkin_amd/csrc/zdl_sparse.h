@@ -57,4 +57,7 @@ hipError_t sparse_accumulate(SparseWork& w, SparseTable& t, uint32_t* log, uint6
 hipError_t sparse_add(SparseWork& w, SparseTable& t, const uint32_t* cells, const unsigned long long* call,
                       const unsigned long long* err, uint64_t n, int cell_bits, hipStream_t s);
 
+// Capacity for n entries in t (its contents are dropped when it grows).
+hipError_t sparse_reserve(SparseTable& t, size_t n);
+
 }  // namespace zdl

@@ -402,6 +402,8 @@ hipError_t sparse_accumulate(SparseWork& w, SparseTable& t, uint32_t* log, uint6
   return merge_into(w, t, w.bcell, w.bcall, w.berr, U, s);
 }
 
+hipError_t sparse_reserve(SparseTable& t, size_t n) { return ensure_table(t, n); }
+
 hipError_t sparse_add(SparseWork& w, SparseTable& t, const uint32_t* cells, const unsigned long long* call,
                       const unsigned long long* err, uint64_t n, int cell_bits, hipStream_t s) {
   if (n == 0) return hipSuccess;

@@ -3,8 +3,9 @@
 Traces are independent, so each rank links its own traces; the low 64 bits of
 the trace id pick the rank, because getDependencies groups by lowTraceId
 (InMemoryStorage.java:163, 330, 465-467): sharding on the full 128-bit id
-would split mixed 64/128-bit traces. The only exchange is one sum of the
-per-rank S x S count tables (DependencyLinker.merge semantics, :189-204).
+would split mixed 64/128-bit traces. The only exchange is the combine of the
+ranks' counts inside libzdl (DependencyLinker.merge semantics, :189-204;
+zipkin_amd/csrc/zdl_xport.inc).
 """
 from __future__ import annotations
 
@@ -23,15 +24,6 @@ def splitmix64(x: np.ndarray) -> np.ndarray:
 
 def shard_of(trace_lo: np.ndarray, n_shards: int) -> np.ndarray:
     return (splitmix64(trace_lo) % np.uint64(n_shards)).astype(np.int64)
-
-
-def combine_tables(call, err, group=None):
-    """Sums per-rank int64 S x S tables in place (torch tensors) with one all-reduce each:
-    RCCL over xGMI on GPUs, gloo on CPU."""
-    import torch.distributed as dist
-    dist.all_reduce(call, op=dist.ReduceOp.SUM, group=group)
-    dist.all_reduce(err, op=dist.ReduceOp.SUM, group=group)
-    return call, err
 
 
 def partition_columns(cols, n_shards: int):
