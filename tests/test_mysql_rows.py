@@ -86,7 +86,7 @@ def as_tuples(links):
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", CASES, ids=lambda c: c[0])
 def test_gpu_iterator_cases_under_a_root(case):
-    from zipkin_amd.mysql import aggregate_dependencies
+    from zipkin_amd.linker import aggregate_dependencies
     rows = with_root(case[1])
     assert as_tuples(aggregate_dependencies(rows)) == as_tuples(M.aggregate_dependencies(rows))
 
@@ -94,7 +94,7 @@ def test_gpu_iterator_cases_under_a_root(case):
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed", range(20))
 def test_gpu_random_rows_vs_oracle(seed):
-    from zipkin_amd.mysql import aggregate_dependencies
+    from zipkin_amd.linker import aggregate_dependencies
     r = random.Random(seed)
     rows = rand_rows(r, r.randrange(1, 300))
     assert as_tuples(aggregate_dependencies(rows)) == as_tuples(M.aggregate_dependencies(rows))

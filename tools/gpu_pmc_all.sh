@@ -2,7 +2,7 @@
 # Per-kernel HBM traffic for every kernel of the C3 shard, C5 and the two decoders: for each
 # command one rocprofv3 --kernel-trace --stats run (durations) and two PMC runs (FETCH_SIZE,
 # WRITE_SIZE), joined by tools/kernel_hbm.py into gpurun_out/hbm_<name>_<TAG>.{txt,json}.
-# (C2's kernels: tools/gpu_round.sh's pmc_fetch / pmc_write passes.)
+# (C2's k_link: bench.py's own FETCH_SIZE / WRITE_SIZE passes, roofline.traffic.)
 #   tools/gpu_pmc_all.sh TAG
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp

@@ -248,3 +248,21 @@ class DependencyLinker:
         if self._ctx is not None:
             self._ctx.close()
             self._ctx = None
+
+
+def aggregate_dependencies(rows, device: int = 0) -> List[DependencyLink]:
+    """mysql-v1's getDependencies after its query: AggregateDependencies.apply
+    (zipkin-storage/mysql-v1/src/main/java/zipkin2/storage/mysql/v1/AggregateDependencies.java:55-84)
+    over the SQL cursor's rows (spans left-joined with their lc/cs/ca/sr/sa/error annotations,
+    grouped by trace then span id): DependencyLinkV2SpanIterator's projection and the linking
+    on the device (zdl_put_mysql_rows), DependencyLinker.link()'s order.
+
+    rows: (trace_id_high, trace_id, parent_id, id, a_key, a_type, endpoint_service_name)."""
+    rows = list(rows)
+    if not rows:  # !traces.hasNext() -> emptyList
+        return []
+    linker = DependencyLinker(device)
+    try:
+        return linker.put_mysql_rows(rows).link()
+    finally:
+        linker.close()
