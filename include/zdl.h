@@ -400,9 +400,15 @@ void zdl_shard_of(const uint64_t* trace_lo, uint64_t n, uint32_t n_shards, uint3
  * flooredTraceTimestamp rule over its spans in storage order (:680-690), with `timestamp`
  * holding guessTimestamp (Span.timestamp, else the first annotation's, :692-700) - for the
  * n_days (<= 255) UTC days from day0_ms (a midnight). A trace without a timestamp or
- * outside the range fails the put (ZDL_EINVAL). Resets the counts; n_days = 0 turns it off.
- * Not with a time window. Tables hold n_days * S * S cells; zdl_table_export/import move
- * all of them. zdl_link is refused while days are set: */
+ * outside the range fails the put (ZDL_EINVAL); with ZDL_DAYS_SKIP_OUTSIDE or-ed into n_days
+ * a trace whose day lies outside the range is skipped instead (a caller covers a long span
+ * of days by putting the same batch once per range of days). Resets the counts; n_days = 0
+ * turns it off. Not with a time window. Dense and hash tables hold n_days * S * S cells
+ * (< 2^32); zdl_table_export/import move all of them. A sparse context (above 1024 services)
+ * keeps its one sorted list with the day in the cell - (day * S + parent) * S + child, below
+ * 2^31 - so no table is allocated per day; it links in ZDL_ORDER_SORTED only. zdl_link is
+ * refused while days are set: */
+#define ZDL_DAYS_SKIP_OUTSIDE 0x80000000u
 int zdl_set_days(zdl_ctx* ctx, int64_t day0_ms, uint32_t n_days);
 
 typedef struct zdl_day_links {

@@ -165,3 +165,100 @@ def test_gpu_daily_sparse_day_ranges(seed, monkeypatch):
     got = daily.aggregate_links(out)
     assert _as_lists(got) == _as_lists(O.aggregate_links(out))
     assert 0 in got and len(got) >= 8
+
+
+def _assert_same_days(got, want):
+    g, w = dict(_as_sorted_sets(got)), dict(_as_sorted_sets(want))
+    assert sorted(g) == sorted(w)
+    for d in w:
+        a, b = set(g[d]), set(w[d])
+        assert a == b, (d, len(a), len(b), sorted(a - b)[:5], sorted(b - a)[:5])
+
+
+def _as_sorted_sets(d):
+    return sorted((day, sorted((l.parent, l.child, l.call_count, l.error_count) for l in ls)) for day, ls in d.items())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(12))
+def test_gpu_daily_sorted_device_grouped_vs_oracle(seed):
+    """insertion_order=False: no host grouping - the spans go to the device in arrival order
+    and are grouped by low trace id there; per day the same links as the oracle's linkers."""
+    from zipkin_amd.daily import aggregate_links
+    sp = _multi_day_spans(500 + seed)
+    got = aggregate_links(sp, insertion_order=False)
+    assert list(got) == sorted(got)  # days ascending
+    for ls in got.values():
+        assert [(l.parent, l.child) for l in ls] == sorted((l.parent, l.child) for l in ls)
+    assert _as_sorted_sets(got) == _as_sorted_sets(O.aggregate_links(sp))
+
+
+def _high_cardinality_spans(seed, n_traces, n_services, days):
+    """random_trace shapes whose service names are drawn per trace from a pool of
+    n_services names, spread over `days` days (some spans timed only by an annotation)."""
+    r = random.Random(seed)
+    from tests.stress import SVCS
+    base = 1_704_067_200_000_000
+    pool = [f"svc-{k:05d}" for k in range(n_services)]
+    out = []
+    for _ in range(n_traces):
+        t = random_trace(r, allow_npe=False)
+        tid = format(r.getrandbits(64) | 1, "016x")
+        day = r.randrange(days)
+        names = dict(zip(SVCS, r.sample(pool, len(SVCS))))
+        ren = lambda e: None if e is None else e.__class__(names.get(e.service_name, e.service_name) if e.service_name
+                                                           else None, e.ipv4, e.ipv6, e.port)  # noqa: E731
+        for s in t:
+            ts = base + day * DAY * 1000 + r.randrange(DAY * 1000)
+            ann = ()
+            if r.random() < 0.2:
+                ann, ts = ((ts, "sr"),), 0
+            out.append(s.to_builder(trace_id=tid, timestamp=ts, annotations=ann,
+                                    local_endpoint=ren(s.local_endpoint), remote_endpoint=ren(s.remote_endpoint)))
+    r.shuffle(out)
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(3))
+def test_gpu_daily_sparse_10k_services_5_days(seed):
+    """10 000 services over 5 days: a sparse context (no days x S x S table; the day rides in
+    the sorted list's cell) against the oracle pinned by ITDependencies."""
+    from zipkin_amd import daily
+    sp = _high_cardinality_spans(900 + seed, 2500, 10_000, 5)
+    n_svc = len({e.service_name for s in sp for e in (s.local_endpoint, s.remote_endpoint) if e is not None})
+    assert n_svc >= daily.SPARSE_MIN_SERVICES
+    got = daily.aggregate_links(sp, insertion_order=False)
+    want = O.aggregate_links(sp)
+    assert len(got) == 5
+    _assert_same_days(got, want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sparse", [False, True])
+def test_gpu_daily_sorted_skips_other_ranges(sparse, monkeypatch):
+    """Days far apart (and a trace floored to 1970 by the micros-vs-millis quirk) in ranges of
+    at most 2 days: one pass per range over the same device batch, each skipping the traces of
+    the other ranges (ZDL_DAYS_SKIP_OUTSIDE); every trace is counted once."""
+    from zipkin_amd import daily
+    if sparse:  # a sparse context at 9 services (ZDL_SPARSE=1), at most 2 days of cells
+        monkeypatch.setenv("ZDL_SPARSE", "1")
+        monkeypatch.setattr(daily, "SPARSE_MIN_SERVICES", 2)
+        monkeypatch.setattr(daily, "SPARSE_CELLS", 2 * 9 * 9 + 1)
+    else:
+        monkeypatch.setattr(daily, "TABLE_BUDGET_BYTES", 16 * 67 * 67 * 2)
+    r = random.Random(31 + sparse)
+    base = 1_704_067_200_000_000
+    out = []
+    for _ in range(80):
+        t = random_trace(r, allow_npe=False)
+        tid = format(r.getrandbits(64) | 1, "016x")
+        day = r.choice([0, 1, 2, 40, 41, 300, 301, 302, 303])
+        for s in t:
+            out.append(s.to_builder(trace_id=tid, timestamp=base + day * DAY * 1000 + r.randrange(DAY * 1000)))
+    q = random_trace(r, n=3, allow_npe=False)  # span 2 is 5 s after the epoch: the trace floors to 0
+    out += [s.to_builder(trace_id="00000000000000e1", timestamp=ts) for s, ts in zip(q, [base, 5_000_000, base + 7])]
+    r.shuffle(out)
+    got = daily.aggregate_links(out, insertion_order=False)
+    assert 0 in got and len(got) >= 8
+    assert _as_sorted_sets(got) == _as_sorted_sets(O.aggregate_links(out))

@@ -20,6 +20,7 @@ ZDL_DICT_SERVICE, ZDL_DICT_IPV4, ZDL_DICT_IPV6 = 0, 1, 2
 # JSON v2 keys (include/zdl.h): raw service token text, ipv4 text, ipv6 text (missing list only)
 ZDL_DICT_JSON_SERVICE, ZDL_DICT_JSON_IPV4, ZDL_DICT_JSON_IPV6TEXT = 3, 4, 5
 ZDL_ORDER_SORTED, ZDL_ORDER_FIRST_SEEN, ZDL_ORDER_INSERTION = 0, 1, 2
+ZDL_DAYS_SKIP_OUTSIDE = 0x80000000
 ZDL_FLAG_TIMING = 1
 ZDL_FLAG_TIMING_ALL = 2
 ZDL_FLAG_INSERTION_ORDER = 4
@@ -422,9 +423,11 @@ class Context:
         self.check(self._L.zdl_link_finish(self.h, C.byref(out)))
         return self._links_to_numpy(out, copy)
 
-    def set_days(self, day0_ms: int, n_days: int):
-        """Daily buckets (zdl_set_days): the timestamp column then holds guessTimestamp."""
-        self.check(self._L.zdl_set_days(self.h, int(day0_ms), int(n_days)))
+    def set_days(self, day0_ms: int, n_days: int, skip_outside: bool = False):
+        """Daily buckets (zdl_set_days): the timestamp column then holds guessTimestamp.
+        skip_outside: traces whose day lies outside the range are skipped (ZDL_DAYS_SKIP_OUTSIDE)."""
+        self.check(self._L.zdl_set_days(self.h, int(day0_ms), int(n_days) | (ZDL_DAYS_SKIP_OUTSIDE if skip_outside
+                                                                                 else 0)))
 
     def link_days(self, order: int = ZDL_ORDER_SORTED):
         """(days, day, parent, child, call, err): the days holding a trace, then per link."""

@@ -60,6 +60,15 @@ constexpr int wtable_bytes(int window) { return window ? WTABLE_BYTES_WINDOW : W
 // k_scatter group the log by partition, k_hist counts each partition in a dense LDS table.
 constexpr int PSHIFT = 12;          // cells per partition: 4096 u64 LDS cells = 32 KB in k_hist
 constexpr int PMAX = 256;           // partitions (per-wave LDS counters in k_link): S <= 1024
+// ZDL_LOG_ROWS (round 5; 0 = round 4's reduce, for A/B builds): k_link writes ONE partition-count
+// row per workgroup (its waves summed in LDS), k_scatter2 takes one k_link workgroup's segments
+// in order - so a partition's entries of consecutive segments land in ONE contiguous run (the
+// prefix runs over 512 rows instead of 8192 waves) - and ranks a wave's entries per partition by
+// ballot masks (one LDS atomic per partition a wave holds, not one per entry); k_hist2 runs one
+// 1024-thread workgroup per CU (fewer flushes of each partition's cells).
+#ifndef ZDL_LOG_ROWS
+#define ZDL_LOG_ROWS 1
+#endif
 // k_link's table modes (template parameter DENSE): hash, dense, log
 constexpr int TM_HASH = 0, TM_DENSE = 1, TM_LOG = 2;
 // SORT (sparse contexts, zdl_sparse.h): k_link logs every link like LOG, without partition
@@ -139,6 +148,7 @@ struct Args {
   // day_first[d] = put-global position of day d's first trace
   uint32_t rows;
   uint32_t days;
+  uint32_t days_skip;  // ZDL_DAYS_SKIP_OUTSIDE: a trace outside the days is skipped, not an error
   int64_t day0;
   unsigned long long* day_first;
   unsigned long long* o_key;
@@ -199,6 +209,7 @@ constexpr int CTR_DONE = 2 * CTR_N;  // k_tail's finished-workgroup count (after
 #include "zdl_full.inc"  // the full per-window emulation (k_tail's first part)
 constexpr unsigned long long FLAG_TAIL = 1ull << 62;  // lazy put: k_mid / k_tail still have work
 __device__ void lk_lazy_end(const Args& A, uint32_t* scratch);  // k_link's end in a lazy put (below)
+__device__ void lk_lazy_end_log(const Args& A, uint32_t* scratch);  // ... of a LOG-mode put
 #include "zdl_link.inc"  // k_link, full_windows (need zdl_full.inc's helpers)
 #include "zdl_log.inc"   // LOG mode reduce: k_pscan, k_scatter, k_hist
 
@@ -1128,8 +1139,8 @@ __device__ __forceinline__ bool big_one(const Args& A, unsigned char* lds, size_
         sh_act = 1;
         const int64_t d = m == INT64_MAX ? -1 : (m - A.day0) / DAY_MS;
         const bool ok = m != INT64_MAX && m >= A.day0 && d < (int64_t)A.days;
-        if (!ok) atomicOr(A.status, ST_DAYS);
-        else ord_min(&A.day_first[d], A.span_base + b);
+        if (!ok && (m == INT64_MAX || !A.days_skip)) atomicOr(A.status, ST_DAYS);
+        else if (ok) ord_min(&A.day_first[d], A.span_base + b);
         sh_ts_min = ok ? d : -1;
       }
       big_sync();
@@ -1267,6 +1278,37 @@ __device__ void lk_lazy_end(const Args& A0, uint32_t* scratch) {
   }
 }
 
+// A lazy LOG-mode put's k_link end (round 5): the same ticket as lk_lazy_end, but nothing to
+// compact (large tables are compacted on the device at zdl_link, after the LOG reduce). If k_link
+// left nothing for k_mid / k_big / k_tail, the last workgroup zeroes the next put's counter
+// slots and stores `seq`: the put is k_link and the LOG reduce (its kernels already queued), and
+// the tail kernels, five near-empty launches a step, are never launched.
+__device__ void lk_lazy_end_log(const Args& A0, uint32_t* scratch) {
+  KArgs& A = rare(A0);
+  uint32_t& last = scratch[0];
+  uint32_t& tail = scratch[1];
+  __syncthreads();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    last = __hip_atomic_fetch_add(A.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  if (threadIdx.x == 0) {
+    const uint32_t b = __hip_atomic_load(A.big_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t l = __hip_atomic_load(A.large_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t x = __hip_atomic_load(A.cx_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    tail = (b | l | x) != 0;
+  }
+  __syncthreads();
+  if (!tail && threadIdx.x < CTR_N) A.ctr_next[threadIdx.x] = 0;  // k_tail's job when it runs
+  if (threadIdx.x == 0) {
+    *A.done = 0;
+    __threadfence_system();
+    __hip_atomic_store(A.flag, tail ? (A.seq | FLAG_TAIL) : A.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 __global__ void __launch_bounds__(COMPACT_WG) k_compact_ordered(const unsigned long long* __restrict__ call,
                                                                 const unsigned long long* __restrict__ err,
                                                                 uint32_t SS, uint32_t S,
@@ -1389,7 +1431,8 @@ __global__ void __launch_bounds__(NT, NT == 256 ? 4 : 1) k_big(Args A) {
 }
 
 inline const void* k_tail_fn(int dense, int window, int ord = 0) {  // dense: 0 hash, 1 dense, 2 sparse sink
-  if (dense == 2) return window ? (const void*)k_tail<2, 1, 0> : (const void*)k_tail<2, 0, 0>;
+  if (dense == 2)  // (daily buckets on a sparse context: the day rides in the logged cell)
+    return window == 2 ? (const void*)k_tail<2, 2, 0> : window ? (const void*)k_tail<2, 1, 0> : (const void*)k_tail<2, 0, 0>;
   if (window == 2) {  // daily buckets
     if (ord) return dense ? (const void*)k_tail<1, 2, 1> : (const void*)k_tail<0, 2, 1>;
     return dense ? (const void*)k_tail<1, 2, 0> : (const void*)k_tail<0, 2, 0>;
@@ -1579,6 +1622,7 @@ struct zdl_ctx {
   bool ord = false;
   // daily buckets (zdl_set_days): the tables hold rows = days * S parent rows
   uint32_t days = 0, rows = 0;
+  bool days_skip = false;
   int64_t day0 = 0;
   DevBuf<unsigned long long> day_first;
   std::vector<unsigned long long> h_day_first;
@@ -1677,7 +1721,7 @@ struct zdl_ctx {
   DevBuf<int32_t> o_p, o_c;
   DevBuf<int64_t> o_call, o_err;
   DevBuf<ZLink> o_links;
-  uint64_t* h_meta = nullptr;  // pinned: link count, status
+  uint64_t* h_meta = nullptr;  // pinned (8 words): link count, status; sparse_finish's counts
   unsigned long long* h_map = nullptr;  // mapped pinned: status, count, ordered records
   unsigned long long* h_ordmap = nullptr;  // mapped pinned: insertion order's records (k_ord_compact)
   unsigned long long* d_ordmap = nullptr;
@@ -1910,7 +1954,7 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
   if (e == hipSuccess && c->ord) e = hipMemsetAsync(c->first.p, 0xff, SS * 8, c->stream);
   if (e == hipSuccess) e = c->counters.ensure(CTR_DONE + 1);  // + k_tail's finished-workgroup count
   if (e == hipSuccess) e = hipMemsetAsync(c->counters.p, 0, (CTR_DONE + 1) * 4, c->stream);
-  if (e == hipSuccess) e = hipHostMalloc((void**)&c->h_meta, 16, hipHostMallocDefault);
+  if (e == hipSuccess) e = hipHostMalloc((void**)&c->h_meta, 64, hipHostMallocDefault);
   // timing-only events: no system-scope fence (cache writeback) between the kernels they bracket
   for (int i = 0; i < 12 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->ev[i], hipEventDisableSystemFence);
   for (int i = 0; i < 2 * zdl_ctx::LK_RING && e == hipSuccess && (cfg->flags & ZDL_FLAG_TIMING); ++i)
@@ -1937,9 +1981,9 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
                             (int)std::max(tail_block_bytes(0), std::max(tail_block_bytes(1), tail_block_bytes(2))));
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)k_big<256>, hipFuncAttributeMaxDynamicSharedMemorySize, KB_SMALL_LDS);
-  for (int d = 0; d < 2 && e == hipSuccess; ++d)
+  for (int d = 0; d < 3 && e == hipSuccess; ++d)
     for (int w = 0; w < 3 && e == hipSuccess; ++w)
-      for (int o = 0; o < 2 && e == hipSuccess; ++o)
+      for (int o = 0; o < (d == 2 ? 1 : 2) && e == hipSuccess; ++o)
         e = hipFuncSetAttribute(k_tail_fn(d, w, o), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)tail_block_bytes(w));
   for (int w = 0; w < 2 && e == hipSuccess; ++w) {
@@ -2119,20 +2163,25 @@ int zdl_set_days(zdl_ctx* c, int64_t day0_ms, uint32_t n_days) {
   if (c->link_pending >= 0) return fail(c, ZDL_EINVAL, "zdl_set_days: a started link is not finished (zdl_link_finish)");
   if (const int frc = stage_flush(c)) return frc;  // staged putTrace calls come first
   if (!c->sub.empty() || in_job(c)) return fail(c, ZDL_EINVAL, "zdl_set_days: one device, one process");
-  if (c->sparse) return fail(c, ZDL_EINVAL, "zdl_set_days: needs the S x S table (a sparse context has none)");
+  const bool skip = (n_days & ZDL_DAYS_SKIP_OUTSIDE) != 0;
+  n_days &= ~ZDL_DAYS_SKIP_OUTSIDE;
   if (n_days > 255) return fail(c, ZDL_EINVAL, "zdl_set_days: at most 255 days");
   if (n_days && (day0_ms % DAY_MS) != 0) return fail(c, ZDL_EINVAL, "zdl_set_days: day0 must be a UTC midnight");
   if (n_days && c->window) return fail(c, ZDL_EINVAL, "zdl_set_days: not with a time window");
-  if ((uint64_t)(n_days ? n_days : 1) * c->S * c->S >= (1ull << 32))
-    return fail(c, ZDL_EINVAL, "zdl_set_days: days * S * S must stay below 2^32");
+  // a sparse context's cells are u32 log entries (cell << 1 | error): the day rides in the cell
+  const uint64_t cells = (uint64_t)(n_days ? n_days : 1) * c->S * c->S;
+  if (c->sparse && cells >= (1ull << 31))
+    return fail(c, ZDL_EINVAL, "zdl_set_days: a sparse context needs days * S * S below 2^31");
+  if (cells >= (1ull << 32)) return fail(c, ZDL_EINVAL, "zdl_set_days: days * S * S must stay below 2^32");
   HIP_TRY(c, enter(c));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   c->days = n_days;
+  c->days_skip = n_days && skip;
   c->day0 = n_days ? day0_ms : 0;
   c->rows = (n_days ? n_days : 1) * c->S;
-  const size_t SS = (size_t)c->rows * c->S;
-  HIP_TRY(c, c->call.ensure(SS));
-  HIP_TRY(c, c->errc.ensure(SS));
+  const size_t SS = c->sparse ? 0 : (size_t)c->rows * c->S;  // sparse: one list, no table
+  if (SS) HIP_TRY(c, c->call.ensure(SS));
+  if (SS) HIP_TRY(c, c->errc.ensure(SS));
   if (c->ord) HIP_TRY(c, c->first.ensure(SS));
   if (n_days) HIP_TRY(c, c->day_first.ensure(n_days));
   c->map_fresh = false;
@@ -2258,15 +2307,21 @@ __global__ void __launch_bounds__(256) k_seg_copy(const uint32_t* __restrict__ l
 }
 
 static int sparse_finish(zdl_ctx* c, uint32_t ep, uint32_t lW, uint64_t n_spans, uint64_t n_traces,
-                         const uint64_t* off) {
+                         const uint64_t* off, const uint64_t* n_traces_dev, bool slots) {
   const hipStream_t s = c->stream;
   // how many big traces and queued windows k_tail logged (this put's counter slots)
   HIP_TRY(c, hipMemcpyAsync(c->h_meta, c->counters.p + ep * CTR_N, 4 * (CTR_LARGE + 1), hipMemcpyDeviceToHost, s));
+  if (n_traces_dev) HIP_TRY(c, hipMemcpyAsync(c->h_meta + 2, n_traces_dev, 8, hipMemcpyDeviceToHost, s));
   HIP_TRY(c, hipStreamSynchronize(s));
-  const uint32_t nb = ((uint32_t*)c->h_meta)[CTR_MID], nw = ((uint32_t*)c->h_meta)[CTR_CX],
-                 nl = ((uint32_t*)c->h_meta)[CTR_LARGE];
+  // (grouped on the device: n_traces is an upper bound - big_list's capacity - and the count is
+  // the device's)
+  const uint64_t n_dev = n_traces_dev ? std::min<uint64_t>(n_traces, c->h_meta[2]) : n_traces;
+  const uint32_t nb = ((uint32_t*)c->h_meta)[CTR_MID], nl = ((uint32_t*)c->h_meta)[CTR_LARGE];
+  // k_link mode 3 (plan only: daily buckets) queues a slot per trace, not a counted queue
+  const uint32_t nw = slots ? (uint32_t)n_dev : ((uint32_t*)c->h_meta)[CTR_CX];
   if ((uint64_t)nb + nl > n_traces || nw > n_traces) return fail(c, ZDL_EDEVICE, "sparse: inconsistent tail counters");
   const uint64_t nseg = (uint64_t)lW + nb + nl + nw;
+  if (nseg == 0) return ZDL_OK;
   HIP_TRY(c, c->seg_src.ensure(nseg));
   HIP_TRY(c, c->seg_n.ensure(nseg));
   HIP_TRY(c, c->seg_off.ensure(nseg));
@@ -2290,7 +2345,7 @@ static int sparse_finish(zdl_ctx* c, uint32_t ep, uint32_t lW, uint64_t n_spans,
                      c->seg_src.p, c->seg_n.p, c->seg_off.p, nseg, E, c->lin.p);
   HIP_TRY(c, hipGetLastError());
   int kb = 1;
-  while ((1ull << kb) < (uint64_t)c->S * c->S) ++kb;
+  while ((1ull << kb) < (uint64_t)c->rows * c->S) ++kb;  // daily buckets: the day rides in the cell
   HIP_TRY(c, sparse_accumulate(c->sw, c->acc, c->lin.p, E, kb + 1, s));
   return ZDL_OK;
 }
@@ -2495,6 +2550,7 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   A.window = c->window;
   A.rows = c->rows;
   A.days = c->days;
+  A.days_skip = c->days_skip ? 1u : 0u;
   A.day0 = c->day0;
   A.day_first = c->day_first.p;
   const int wmode = c->days ? 2 : c->window;  // k_tail's timestamp mode
@@ -2660,26 +2716,42 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
     A.o_bfs = c->o_bfs.p;
   }
   const bool ordered = SS <= (size_t)COMPACT_WG * 8 && !c->ord && !c->days && !c->sparse;
-  if (ordered) HIP_TRY(c, ensure_map(c));
+  static const bool nolazy = getenv("ZDL_NOLAZY") != nullptr;
+  // a lazy LOG put (round 5): k_mid / k_big / k_tail only when k_link's flag asks for them
+  const bool lazy_log = tm == TM_LOG && lmode == 0 && !c->ord && !c->days && !nolazy &&
+                        !(c->flags & ZDL_FLAG_TIMING_ALL);
+  if (ordered || lazy_log) HIP_TRY(c, ensure_map(c));
   A.map = ordered && !getenv("ZDL_NOTAILMAP") ? c->d_map : nullptr;
   A.done = c->counters.p + CTR_DONE;
-  if (A.map) {
+  if (A.map || lazy_log) {
     A.flag = c->d_flag;
     A.seq = c->seq + 1;
   }
   // lazy put (small dense tables, the production k_link): k_link's last workgroup compacts when
   // nothing is left for k_mid / k_tail, which then are not launched (resolve_lazy launches them
   // when its flag says so)
-  static const bool nolazy = getenv("ZDL_NOLAZY") != nullptr;
-  A.lazy = A.map && tm == TM_DENSE && lmode == 0 && !nolazy && !(c->flags & ZDL_FLAG_TIMING_ALL) ? 1 : 0;
+  A.lazy = (A.map && tm == TM_DENSE && lmode == 0 && !nolazy && !(c->flags & ZDL_FLAG_TIMING_ALL)) || lazy_log ? 1 : 0;
   void* kargs[] = {&A};
   ev_record(c, 0);
   ev_record(c, 1);
   // A failed launch poisons nothing yet either: no kernel of this put ran
+  // (mode 3 on a sparse context runs the hash instantiation, k_link_fn: its LDS holds the table)
   HIP_TRY(c, hipLaunchKernel(k_link_fn(tm, c->window, lmode), dim3(lgrid), dim3(lk::waves(c->window, lmode) * 64), kargs,
-                             link_block_bytes(lmode == 3 ? 0 : c->window, tm, lmode), c->stream));
+                             link_block_bytes(lmode == 3 ? 0 : c->window, lmode == 3 && tm == TM_SORT ? TM_HASH : tm,
+                                              lmode),
+                             c->stream));
   ev_record(c, 7);
   if (tm == TM_LOG) {  // group the log by partition, count each partition in LDS (zdl_log.inc)
+#if ZDL_LOG_ROWS
+    // rows = k_link's workgroups (the column prefix over 512 rows), a scatter workgroup per row
+    hipLaunchKernelGGL(k_pscan, dim3(lP), dim3(PSCAN_WG), 0, c->stream, c->lg_cnt.p, (uint32_t)lgrid, lP, c->lg_tot.p);
+    hipLaunchKernelGGL(k_pbase, dim3(1), dim3(PMAX), 0, c->stream, c->lg_tot.p, lP, c->lg_tot.p + PMAX);
+    hipLaunchKernelGGL(k_scatter2, dim3((unsigned)lgrid), dim3(SCATTER2_WG), 0, c->stream, c->lg.p, c->lg_start.p,
+                       c->lg_n.p, c->lg_cnt.p, (uint32_t)lk::waves(c->window, lmode), lP, c->lg_tot.p + PMAX,
+                       c->lg_grp.p);
+    hipLaunchKernelGGL(k_hist2, dim3((unsigned)c->cus), dim3(HIST2_WG), 0, c->stream, c->lg_grp.p,
+                       c->lg_tot.p + PMAX, lP, (uint64_t)SS, c->call.p, c->errc.p);
+#else
     hipLaunchKernelGGL(k_pscan, dim3(lP), dim3(PSCAN_WG), 0, c->stream, c->lg_cnt.p, lW, lP, c->lg_tot.p);
     hipLaunchKernelGGL(k_pbase, dim3(1), dim3(PMAX), 0, c->stream, c->lg_tot.p, lP, c->lg_tot.p + PMAX);
     hipLaunchKernelGGL(k_scatter, dim3((unsigned)std::min<uint32_t>(lW, (uint32_t)c->cus * 8)), dim3(SCATTER_WG), 0,
@@ -2687,6 +2759,7 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
                        c->lg_grp.p);
     hipLaunchKernelGGL(k_hist, dim3((unsigned)c->cus * 4), dim3(HIST_WG), 0, c->stream, c->lg_grp.p,
                        c->lg_tot.p + PMAX, lP, (uint64_t)SS, c->call.p, c->errc.p);
+#endif
     const hipError_t ke = hipGetLastError();
     if (ke != hipSuccess) {
       c->poisoned = true;
@@ -2703,7 +2776,7 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
     c->seq = A.seq;
     c->span_base += n_spans;
     ++c->epoch;  // k_link's last workgroup (or k_tail) zeroes the other counter slots
-    c->map_fresh = true;
+    c->map_fresh = tm == TM_DENSE;  // (a LOG put compacts nothing into the mapped buffer)
     c->times.grid = (uint32_t)grid;
     return ZDL_OK;
   }
@@ -2768,7 +2841,8 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   }
   ev_record(c, 4);
   if (c->sparse) {  // gather the put's log segments, sort, reduce and merge into the list
-    const int rc = sparse_finish(c, ep, lW, n_spans, n_traces, off);
+    // (plan only, k_link mode 3, logs nothing: its k_link instantiation keeps no segments)
+    const int rc = sparse_finish(c, ep, plan_only ? 0u : lW, n_spans, n_traces, off, n_traces_dev, plan_only);
     if (rc != ZDL_OK) {
       c->span_base += n_spans;
       ++c->epoch;
@@ -3837,60 +3911,15 @@ int zdl_link_finish(zdl_ctx* c, zdl_links* out) {
 
 // Daily buckets: the cells as (day, parent, child, counts), ordered like
 // ITDependencies.aggregateLinks' map of per-day DependencyLinker.link() lists.
-int zdl_link_days(zdl_ctx* c, int order, zdl_day_links* out) {
-  if (!c || !out) return ZDL_EINVAL;
-  if (c->link_pending >= 0) return fail(c, ZDL_EINVAL, "zdl_link_days: a started link is not finished (zdl_link_finish)");
-  if (const int frc = stage_flush(c)) return frc;  // staged putTrace calls come first
-  if (!c->sub.empty() || in_job(c)) return fail(c, ZDL_EINVAL, "zdl_link_days: one device, one process");
-  if (!c->days) return fail(c, ZDL_EINVAL, "zdl_link_days: no daily buckets (zdl_set_days)");
-  if (order == ZDL_ORDER_INSERTION && !c->ord)
-    return fail(c, ZDL_EINVAL, "ZDL_ORDER_INSERTION needs a ZDL_FLAG_INSERTION_ORDER context");
-  if (order != ZDL_ORDER_INSERTION && order != ZDL_ORDER_SORTED)
-    return fail(c, ZDL_EINVAL, "zdl_link_days: order must be ZDL_ORDER_SORTED or ZDL_ORDER_INSERTION");
-  HIP_TRY(c, enter(c));
-  const uint64_t SS = (uint64_t)c->rows * c->S;
-  HIP_TRY(c, c->o_p.ensure(SS));
-  HIP_TRY(c, c->o_c.ensure(SS));
-  HIP_TRY(c, c->o_call.ensure(SS));
-  HIP_TRY(c, c->o_err.ensure(SS));
-  HIP_TRY(c, c->o_first.ensure(SS));
-  HIP_TRY(c, hipMemsetAsync(c->count.p, 0, 8, c->stream));
-  if (c->ord) {  // non-zero cells with their first-addLink ranks
-    hipLaunchKernelGGL(k_merge_compact, dim3((unsigned)((SS + 255) / 256)), dim3(256), 0, c->stream, c->call.p,
-                       c->errc.p, c->first.p, SS, c->S, c->count.p, c->o_p.p, c->o_c.p, c->o_call.p, c->o_err.p,
-                       c->o_first.p);
-  } else {
-    HIP_TRY(c, c->o_links.ensure(SS));
-    hipLaunchKernelGGL(k_compact, dim3((unsigned)((SS + 255) / 256)), dim3(256), 0, c->stream, c->call.p, c->errc.p,
-                       SS, c->S, c->count.p, c->o_links.p);
-  }
-  HIP_TRY(c, hipGetLastError());
-  unsigned long long m = 0;
-  HIP_TRY(c, hipMemcpyAsync(&m, c->count.p, 8, hipMemcpyDeviceToHost, c->stream));
-  c->h_day_first.assign(c->days, 0);
-  HIP_TRY(c, hipMemcpyAsync(c->h_day_first.data(), c->day_first.p, (size_t)c->days * 8, hipMemcpyDeviceToHost,
-                            c->stream));
-  const int rc = zdl_sync(c);
-  if (rc != ZDL_OK) return rc;
-  std::vector<int32_t> row(m), ch(m);
-  std::vector<int64_t> ca(m), er(m);
-  std::vector<uint64_t> first(m, 0);
-  if (m && c->ord) {
-    HIP_TRY(c, hipMemcpy(row.data(), c->o_p.p, m * 4, hipMemcpyDeviceToHost));
-    HIP_TRY(c, hipMemcpy(ch.data(), c->o_c.p, m * 4, hipMemcpyDeviceToHost));
-    HIP_TRY(c, hipMemcpy(ca.data(), c->o_call.p, m * 8, hipMemcpyDeviceToHost));
-    HIP_TRY(c, hipMemcpy(er.data(), c->o_err.p, m * 8, hipMemcpyDeviceToHost));
-    HIP_TRY(c, hipMemcpy(first.data(), c->o_first.p, m * 8, hipMemcpyDeviceToHost));
-  } else if (m) {
-    std::vector<ZLink> recs(m);
-    HIP_TRY(c, hipMemcpy(recs.data(), c->o_links.p, m * sizeof(ZLink), hipMemcpyDeviceToHost));
-    for (size_t i = 0; i < m; ++i) {
-      row[i] = recs[i].parent;
-      ch[i] = recs[i].child;
-      ca[i] = recs[i].call;
-      er[i] = recs[i].err;
-    }
-  }
+}  // extern "C"
+
+// The per-day output from (row = day * S + parent, child, counts[, first ranks]) records:
+// sorted by (day, parent, child) in the rank tables' order, or (insertion order) days by their
+// first trace and each day's links by first rank; and the days that hold a trace.
+static int days_out(zdl_ctx* c, int order, std::vector<int32_t>& row, std::vector<int32_t>& ch,
+                    std::vector<int64_t>& ca, std::vector<int64_t>& er, const std::vector<uint64_t>& first,
+                    zdl_day_links* out) {
+  const size_t m = row.size();
   const std::vector<int32_t>& r = c->host_rank[0];
   auto rk = [&](int32_t id) -> int64_t { return (size_t)id < r.size() ? r[id] : id; };
   const uint32_t S = c->S;
@@ -3940,6 +3969,90 @@ int zdl_link_days(zdl_ctx* c, int order, zdl_day_links* out) {
   out->call_count = c->out_call.data();
   out->error_count = c->out_err.data();
   return ZDL_OK;
+}
+
+// A sparse context's daily buckets: its sorted list, cells (day * S + parent) * S + child
+static int link_days_sparse(zdl_ctx* c, int order, zdl_day_links* out) {
+  if (order != ZDL_ORDER_SORTED) return fail(c, ZDL_EINVAL, "zdl_link_days: a sparse context links in ZDL_ORDER_SORTED only");
+  c->h_day_first.assign(c->days, 0);
+  HIP_TRY(c, hipMemcpyAsync(c->h_day_first.data(), c->day_first.p, (size_t)c->days * 8, hipMemcpyDeviceToHost,
+                            c->stream));
+  const int rc = zdl_sync(c);
+  if (rc != ZDL_OK) return rc;
+  const size_t m = c->acc.n;
+  std::vector<uint32_t> cell(m);
+  std::vector<int32_t> row(m), ch(m);
+  std::vector<int64_t> ca(m), er(m);
+  if (m) {
+    HIP_TRY(c, hipMemcpy(cell.data(), c->acc.cell, m * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(c, hipMemcpy(ca.data(), c->acc.call, m * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(c, hipMemcpy(er.data(), c->acc.err, m * 8, hipMemcpyDeviceToHost));
+  }
+  for (size_t i = 0; i < m; ++i) {
+    row[i] = (int32_t)(cell[i] / c->S);
+    ch[i] = (int32_t)(cell[i] % c->S);
+  }
+  return days_out(c, order, row, ch, ca, er, std::vector<uint64_t>(), out);
+}
+
+extern "C" {
+
+int zdl_link_days(zdl_ctx* c, int order, zdl_day_links* out) {
+  if (!c || !out) return ZDL_EINVAL;
+  if (c->link_pending >= 0) return fail(c, ZDL_EINVAL, "zdl_link_days: a started link is not finished (zdl_link_finish)");
+  if (const int frc = stage_flush(c)) return frc;  // staged putTrace calls come first
+  if (!c->sub.empty() || in_job(c)) return fail(c, ZDL_EINVAL, "zdl_link_days: one device, one process");
+  if (!c->days) return fail(c, ZDL_EINVAL, "zdl_link_days: no daily buckets (zdl_set_days)");
+  if (order == ZDL_ORDER_INSERTION && !c->ord)
+    return fail(c, ZDL_EINVAL, "ZDL_ORDER_INSERTION needs a ZDL_FLAG_INSERTION_ORDER context");
+  if (order != ZDL_ORDER_INSERTION && order != ZDL_ORDER_SORTED)
+    return fail(c, ZDL_EINVAL, "zdl_link_days: order must be ZDL_ORDER_SORTED or ZDL_ORDER_INSERTION");
+  HIP_TRY(c, enter(c));
+  if (c->sparse) return link_days_sparse(c, order, out);
+  const uint64_t SS = (uint64_t)c->rows * c->S;
+  HIP_TRY(c, c->o_p.ensure(SS));
+  HIP_TRY(c, c->o_c.ensure(SS));
+  HIP_TRY(c, c->o_call.ensure(SS));
+  HIP_TRY(c, c->o_err.ensure(SS));
+  HIP_TRY(c, c->o_first.ensure(SS));
+  HIP_TRY(c, hipMemsetAsync(c->count.p, 0, 8, c->stream));
+  if (c->ord) {  // non-zero cells with their first-addLink ranks
+    hipLaunchKernelGGL(k_merge_compact, dim3((unsigned)((SS + 255) / 256)), dim3(256), 0, c->stream, c->call.p,
+                       c->errc.p, c->first.p, SS, c->S, c->count.p, c->o_p.p, c->o_c.p, c->o_call.p, c->o_err.p,
+                       c->o_first.p);
+  } else {
+    HIP_TRY(c, c->o_links.ensure(SS));
+    hipLaunchKernelGGL(k_compact, dim3((unsigned)((SS + 255) / 256)), dim3(256), 0, c->stream, c->call.p, c->errc.p,
+                       SS, c->S, c->count.p, c->o_links.p);
+  }
+  HIP_TRY(c, hipGetLastError());
+  unsigned long long m = 0;
+  HIP_TRY(c, hipMemcpyAsync(&m, c->count.p, 8, hipMemcpyDeviceToHost, c->stream));
+  c->h_day_first.assign(c->days, 0);
+  HIP_TRY(c, hipMemcpyAsync(c->h_day_first.data(), c->day_first.p, (size_t)c->days * 8, hipMemcpyDeviceToHost,
+                            c->stream));
+  const int rc = zdl_sync(c);
+  if (rc != ZDL_OK) return rc;
+  std::vector<int32_t> row(m), ch(m);
+  std::vector<int64_t> ca(m), er(m);
+  std::vector<uint64_t> first(m, 0);
+  if (m && c->ord) {
+    HIP_TRY(c, hipMemcpy(row.data(), c->o_p.p, m * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(c, hipMemcpy(ch.data(), c->o_c.p, m * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(c, hipMemcpy(ca.data(), c->o_call.p, m * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(c, hipMemcpy(er.data(), c->o_err.p, m * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(c, hipMemcpy(first.data(), c->o_first.p, m * 8, hipMemcpyDeviceToHost));
+  } else if (m) {
+    std::vector<ZLink> recs(m);
+    HIP_TRY(c, hipMemcpy(recs.data(), c->o_links.p, m * sizeof(ZLink), hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < m; ++i) {
+      row[i] = recs[i].parent;
+      ch[i] = recs[i].child;
+      ca[i] = recs[i].call;
+      er[i] = recs[i].err;
+    }
+  }
+  return days_out(c, order, row, ch, ca, er, first, out);
 }
 
 int zdl_merge_links(zdl_ctx* c, const int32_t* parent, const int32_t* child, const int64_t* call_count,

@@ -158,8 +158,105 @@ void LinkWork::release() {
   cap = 0;
 }
 
+namespace {
+// The non-zero cells of a table up to SEL_MAX cells (LOG mode's S x S <= 2^20), in cell order,
+// by two launches (round 5; hipCUB's DeviceSelect::If took three kernels, ~18 us at C3's 250 000
+// cells): k_sel_count counts each tile's non-zero cells; k_sel_write sums the counts of the tiles
+// before its own (at most SEL_MAX / SEL_TILE of them), scans its tile in the workgroup and writes
+// the indices; the last tile writes the total.
+constexpr int SEL_T = 256, SEL_PER = 16, SEL_TILE = SEL_T * SEL_PER;
+constexpr uint64_t SEL_MAX = 1ull << 22;
+
+__device__ __forceinline__ uint32_t sel_block_sum(uint32_t v, uint32_t* sh) {
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint32_t t = 0;
+  for (int k = 0; k < SEL_T / 64; ++k) t += sh[k];
+  __syncthreads();
+  return t;
+}
+
+__global__ void __launch_bounds__(SEL_T) k_sel_count(const unsigned long long* __restrict__ call, uint32_t SS,
+                                                     uint32_t* __restrict__ tc) {
+  __shared__ uint32_t sh[SEL_T / 64];
+  const uint32_t b0 = blockIdx.x * SEL_TILE;
+  uint32_t n = 0;
+#pragma unroll
+  for (int q = 0; q < SEL_PER; ++q) {
+    const uint32_t i = b0 + q * SEL_T + threadIdx.x;
+    n += (i < SS && call[i] != 0) ? 1u : 0u;
+  }
+  const uint32_t t = sel_block_sum(n, sh);
+  if (threadIdx.x == 0) tc[blockIdx.x] = t;
+}
+
+__global__ void __launch_bounds__(SEL_T) k_sel_write(const unsigned long long* __restrict__ call, uint32_t SS,
+                                                     const uint32_t* __restrict__ tc, uint32_t* __restrict__ sel,
+                                                     uint64_t* __restrict__ count) {
+  __shared__ uint32_t sh[SEL_T / 64];
+  __shared__ uint32_t wsum[SEL_T / 64 + 1];
+  uint32_t before = 0;
+  for (uint32_t k = threadIdx.x; k < blockIdx.x; k += SEL_T) before += tc[k];
+  const uint32_t base = sel_block_sum(before, sh);
+  // thread t takes the SEL_PER consecutive cells [b0 + t * SEL_PER, ...): cell order is thread order
+  const uint32_t c0 = blockIdx.x * SEL_TILE + threadIdx.x * SEL_PER;
+  uint32_t flags = 0;
+#pragma unroll
+  for (int q = 0; q < SEL_PER; ++q) {
+    const uint32_t i = c0 + q;
+    flags |= (i < SS && call[i] != 0) ? (1u << q) : 0u;
+  }
+  const uint32_t mine = (uint32_t)__popc(flags);
+  uint32_t incl = mine;  // inclusive scan over the workgroup
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += y;
+  }
+  if (lane == 63) wsum[wv] = incl;
+  __syncthreads();
+  uint32_t wbase = 0;
+  for (int k = 0; k < wv; ++k) wbase += wsum[k];
+  uint32_t at = base + wbase + incl - mine;
+  for (uint32_t f = flags; f; f &= f - 1) sel[at++] = c0 + (uint32_t)__ffs(f) - 1;
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == SEL_T - 1) *count = (uint64_t)(base + wbase + incl);
+}
+}  // namespace
+
 hipError_t compact_select(LinkWork& w, const unsigned long long* call, uint64_t SS, uint64_t* n_out, hipStream_t s) {
   if (SS == 0 || SS >= (1ull << 32)) return hipErrorInvalidValue;
+  if (SS <= SEL_MAX) {
+    const uint32_t nt = (uint32_t)((SS + SEL_TILE - 1) / SEL_TILE);
+    if (SS > w.cap) {
+      for (int b = 0; b < 2; ++b) {
+        GTRY(grow(w.sel[b], SS));
+        GTRY(grow(w.keys[b], SS));
+      }
+      if (!w.count) GTRY(hipMalloc((void**)&w.count, sizeof(uint64_t)));
+      if (!w.h_count) GTRY(hipHostMalloc((void**)&w.h_count, sizeof(uint64_t), hipHostMallocDefault));
+      size_t b = 0;
+      GTRY(hipcub::DeviceRadixSort::SortPairs(nullptr, b, w.keys[0], w.keys[1], w.sel[0], w.sel[1], (int)SS, 0, 32, s));
+      if (b > w.tmp_bytes) {
+        if (w.tmp) (void)hipFree(w.tmp);
+        w.tmp = nullptr;
+        w.tmp_bytes = 0;
+        GTRY(hipMalloc(&w.tmp, b));
+        w.tmp_bytes = b;
+      }
+      w.cap = SS;
+    }
+    uint32_t* tc = w.keys[1];  // the tile counts (the keys' second buffer is free until the rank sort)
+    hipLaunchKernelGGL(k_sel_count, dim3(nt), dim3(SEL_T), 0, s, call, (uint32_t)SS, tc);
+    GTRY(hipGetLastError());
+    hipLaunchKernelGGL(k_sel_write, dim3(nt), dim3(SEL_T), 0, s, call, (uint32_t)SS, (const uint32_t*)tc, w.sel[0],
+                       w.count);
+    GTRY(hipGetLastError());
+    GTRY(hipMemcpyAsync(w.h_count, w.count, 8, hipMemcpyDeviceToHost, s));
+    GTRY(hipStreamSynchronize(s));
+    *n_out = *w.h_count;
+    return hipSuccess;
+  }
   if (SS > w.cap) {
     for (int b = 0; b < 2; ++b) {
       GTRY(grow(w.sel[b], SS));

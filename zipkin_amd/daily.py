@@ -11,6 +11,13 @@ and a map midnight -> ``DependencyLinker.link()`` in first-seen day order.
 The day of a trace, the per-day (parent, child) counts and the insertion order are
 computed on the device (``zdl_set_days`` / ``zdl_link_days``); the host packs the
 columns with guessTimestamp in the timestamp column and chooses the day range.
+
+Sorted output (``insertion_order=False``) does not group on the host at all: the spans go
+to the device in arrival order and are grouped there by low trace id (the order of traces
+does not change a count), each range of days is one pass over the resident batch that skips
+the traces of other days (ZDL_DAYS_SKIP_OUTSIDE), and above 1024 services the context keeps
+one sparse sorted list with the day in the cell instead of a days x S x S table. Its days come
+back ascending, each day's links sorted by (parent, child) names.
 """
 from __future__ import annotations
 
@@ -87,10 +94,74 @@ def _day_ranges(days: List[int], n_services: int) -> List[List[int]]:
     return out
 
 
+SPARSE_MIN_SERVICES = 1025  # above 1024 services a context keeps a sparse list (zdl_sparse.h)
+SPARSE_CELLS = 1 << 31      # a sparse context's cells (day * S + parent) * S + child stay below this
+
+
+def _span_midnights(ts: np.ndarray) -> np.ndarray:
+    """The UTC midnights of the spans' guessTimestamps (micros; Java's truncating division to
+    millis): a trace's flooredTraceTimestamp is one of them."""
+    t = ts[ts != 0]
+    ms = np.where(t >= 0, t // 1000, -((-t) // 1000))
+    return np.unique((ms // DAY_MS) * DAY_MS)
+
+
+def _ranges(mids: List[int], max_days: int) -> List[List[int]]:
+    out: List[List[int]] = []
+    for d in mids:
+        if out and (d - out[-1][0]) // DAY_MS < max_days:
+            out[-1].append(d)
+        else:
+            out.append([d])
+    return out
+
+
+def _aggregate_sorted(spans: Sequence[Span], device: int) -> Dict[int, List[DependencyLink]]:
+    """aggregate_links(insertion_order=False): device grouping, one pass per range of days."""
+    svc, ip4, ip6 = Dictionary(), Dictionary(), Dictionary()
+    cols = pack_traces([spans], svc, ip4, ip6)  # arrival order; trace_lo per span, grouped on the device
+    cols.timestamp[:] = [guess_timestamp(s) for s in spans]
+    n = max(len(svc), 1)
+    sparse = n >= SPARSE_MIN_SERVICES
+    cap = n if sparse else _capacity(n)  # a sparse context allocates nothing per service
+    if sparse:
+        max_days = max(1, min(255, (SPARSE_CELLS - 1) // (cap * cap)))
+    else:
+        max_days = max(1, min(255, TABLE_BUDGET_BYTES // (16 * cap * cap), ((1 << 32) - 1) // (cap * cap)))
+    mids = [int(d) for d in _span_midnights(cols.timestamp)]
+    if not mids:
+        raise ValueError("a trace has no timestamp (flooredTraceTimestamp asserts one)")
+    rngs = _ranges(mids, max_days)
+    names = svc.strings
+    out: Dict[int, List[DependencyLink]] = {}
+    ctx = N.Context(cap, device)
+    try:
+        ctx.set_ranks(N.ZDL_DICT_SERVICE, svc.ranks())
+        ctx.set_ranks(N.ZDL_DICT_IPV4, ip4.ranks())
+        ctx.set_ranks(N.ZDL_DICT_IPV6, ip6.ranks())
+        for rng in rngs:
+            lo, hi = rng[0], rng[-1]
+            ctx.set_days(lo, (hi - lo) // DAY_MS + 1, skip_outside=len(rngs) > 1)
+            ctx.put_spans_ungrouped(cols)
+            got_days, day, p, c, k, e = ctx.link_days(N.ZDL_ORDER_SORTED)
+            for d in got_days:
+                out.setdefault(int(d), [])
+            for d, a, b, x, y in zip(day.tolist(), p.tolist(), c.tolist(), k.tolist(), e.tolist()):
+                out[int(d)].append(DependencyLink.create(names[a], names[b], int(x), int(y)))
+    finally:
+        ctx.close()
+    return dict(sorted(out.items()))
+
+
 def aggregate_links(spans: Sequence[Span], device: int = 0,
                     insertion_order: bool = True) -> Dict[int, List[DependencyLink]]:
     """midnight (epoch ms) -> that day's links, like ITDependencies.aggregateLinks: the days in
-    first-seen order, each day's links in its linker's order."""
+    first-seen order, each day's links in its linker's order. insertion_order=False: the same
+    links with the days ascending and each day's links sorted by (parent, child)."""
+    if not spans:
+        return {}
+    if not insertion_order:
+        return _aggregate_sorted(spans, device)
     traces = group_by_trace_id(spans)
     if not traces:
         return {}
@@ -110,15 +181,14 @@ def aggregate_links(spans: Sequence[Span], device: int = 0,
         sel = [t for t, d in zip(traces, days) if d in keep]
         cols = pack_traces(sel, svc, ip4, ip6)
         cols.timestamp[:] = [guess_timestamp(s) for t in sel for s in t]
-        ctx = N.Context(cap, device, insertion_order=insertion_order)
+        ctx = N.Context(cap, device, insertion_order=True)
         try:
             ctx.set_ranks(N.ZDL_DICT_SERVICE, svc.ranks())
             ctx.set_ranks(N.ZDL_DICT_IPV4, ip4.ranks())
             ctx.set_ranks(N.ZDL_DICT_IPV6, ip6.ranks())
             ctx.set_days(lo, (hi - lo) // DAY_MS + 1)
             ctx.put_spans(cols)
-            got_days, day, p, c, n, e = ctx.link_days(N.ZDL_ORDER_INSERTION if insertion_order
-                                                      else N.ZDL_ORDER_SORTED)
+            got_days, day, p, c, n, e = ctx.link_days(N.ZDL_ORDER_INSERTION)
         finally:
             ctx.close()
         for d in got_days:
