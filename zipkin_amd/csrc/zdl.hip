@@ -69,6 +69,12 @@ constexpr int PMAX = 256;           // partitions (per-wave LDS counters in k_li
 #ifndef ZDL_LOG_ROWS
 #define ZDL_LOG_ROWS 1
 #endif
+#ifndef ZDL_LOG_ROW_WAVES
+#define ZDL_LOG_ROW_WAVES 4  // k_link waves summed into one row (a divisor of 12 and 16)
+#endif
+#ifndef ZDL_SCATTER_PEERS
+#define ZDL_SCATTER_PEERS 0  // k_scatter2 ranks by ballot masks (1) or by an LDS atomic per entry (0)
+#endif
 // k_link's table modes (template parameter DENSE): hash, dense, log
 constexpr int TM_HASH = 0, TM_DENSE = 1, TM_LOG = 2;
 // SORT (sparse contexts, zdl_sparse.h): k_link logs every link like LOG, without partition
@@ -2744,11 +2750,11 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   if (tm == TM_LOG) {  // group the log by partition, count each partition in LDS (zdl_log.inc)
 #if ZDL_LOG_ROWS
     // rows = k_link's workgroups (the column prefix over 512 rows), a scatter workgroup per row
-    hipLaunchKernelGGL(k_pscan, dim3(lP), dim3(PSCAN_WG), 0, c->stream, c->lg_cnt.p, (uint32_t)lgrid, lP, c->lg_tot.p);
+    const uint32_t rows = lW / ZDL_LOG_ROW_WAVES;
+    hipLaunchKernelGGL(k_pscan, dim3(lP), dim3(PSCAN_WG), 0, c->stream, c->lg_cnt.p, rows, lP, c->lg_tot.p);
     hipLaunchKernelGGL(k_pbase, dim3(1), dim3(PMAX), 0, c->stream, c->lg_tot.p, lP, c->lg_tot.p + PMAX);
-    hipLaunchKernelGGL(k_scatter2, dim3((unsigned)lgrid), dim3(SCATTER2_WG), 0, c->stream, c->lg.p, c->lg_start.p,
-                       c->lg_n.p, c->lg_cnt.p, (uint32_t)lk::waves(c->window, lmode), lP, c->lg_tot.p + PMAX,
-                       c->lg_grp.p);
+    hipLaunchKernelGGL(k_scatter2, dim3(rows), dim3(SCATTER2_WG), 0, c->stream, c->lg.p, c->lg_start.p,
+                       c->lg_n.p, c->lg_cnt.p, (uint32_t)ZDL_LOG_ROW_WAVES, lP, c->lg_tot.p + PMAX, c->lg_grp.p);
     hipLaunchKernelGGL(k_hist2, dim3((unsigned)c->cus), dim3(HIST2_WG), 0, c->stream, c->lg_grp.p,
                        c->lg_tot.p + PMAX, lP, (uint64_t)SS, c->call.p, c->errc.p);
 #else
