@@ -412,6 +412,7 @@ def c5_leg(device, steps=16, parity=True, threads=16, host_threads=2):
     k = c.kernel_times()
     ph = [{"k_link": k.tiles_ms, "k_mid": k.mid_ms, "giant_tier": k.giant_ms, "k_tail": k.big_ms,
            "sparse_merge": k.sparse_ms, "link_compact": k.compact_ms}]
+    sparse_entries = int(k.sparse_entries)
     for c in ctxs:
         c.close()
     del dc, doff, dc2, doff2, bufs
@@ -432,6 +433,13 @@ def c5_leg(device, steps=16, parity=True, threads=16, host_threads=2):
                    "frac": gbs / HBM_PEAK_GBS if gbs else None}
     for k in ("sparse_merge", "link_compact"):
         kern[k] = {"ms": last[k]}
+    # the merge: the put's link log (sparse_entries, 4 B each) read once and the summed list
+    # (cell, call, error: 4 + 8 + 8 B a link) written once
+    sm = last["sparse_merge"]
+    sm_bytes = 4 * sparse_entries + 20 * int(len(out[0]))
+    sm_gbs = sm_bytes / (sm * 1e-3) / 1e9 if sm and sm > 0 else None
+    kern["sparse_merge"].update({"entries": sparse_entries, "algorithmic_bytes": sm_bytes, "achieved_gbs": sm_gbs,
+                                 "frac": sm_gbs / HBM_PEAK_GBS if sm_gbs else None})
     res = {"workload": w.name, "spans": cols.n_spans, "traces": cols.n_traces, "services": S,
            "ms_per_step": ms, "spans_per_s": cols.n_spans / (ms * 1e-3), "inflight": 2, "host_threads": host_threads,
            "ms_per_step_serial": serial_ms,
@@ -788,6 +796,27 @@ def main():
         serial_ms = (time.perf_counter() - t1) / ns * 1e3
         tiles = float(sctx.kernel_times().tiles_ms)
         sctx.close()
+    log_reduce = None
+    if world == 1 and config == "c3":
+        # LOG mode's reduce of k_link's emit log (zdl_log.inc), one put alone with HIP events
+        # around every phase (ZDL_FLAG_TIMING_ALL): priced on its input, 4 B an entry read once
+        pctx = N.Context(S, device=local, timing_all=True)
+        for _ in range(2):
+            launch(pctx)
+            pctx.link(copy=False)
+        pctx.sync()
+        kt = pctx.kernel_times()
+        pctx.close()
+        ent = int(kt.log_entries)
+        rms = float(kt.reduce_ms)
+        gbs = 4 * ent / (rms * 1e-3) / 1e9 if rms > 0 else None
+        log_reduce = {"ms": rms, "entries": ent, "algorithmic_bytes": 4 * ent,
+                      "moved_bytes_model": 12 * ent,
+                      "achieved_gbs": gbs, "frac": gbs / HBM_PEAK_GBS if gbs else None,
+                      "k_link_ms_same_put": float(kt.tiles_ms),
+                      "note": "k_pscan + k_pbase + k_scatter2 + k_hist2 of one put (HIP events); algorithmic: "
+                              "the log read once (4 B/entry); the kernels move 12 B/entry (scatter reads "
+                              "and writes it, hist reads it) plus the per-row partition counts"}
     ctxs = []
     del keep, batches[1:]
     if dist:
@@ -952,6 +981,7 @@ def main():
                                      "k_link_inflight_events": tiles_inflight},
                        "step_roofline_frac": bytes_launch / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
                        "k_link_read_frac": read_launch / (tiles * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                       "log_reduce": log_reduce,
                        "parity": parity, "links": int(len(p)), "insertion_order": ins, "host_buffers": h2d,
                        "proto3_ingest": p3, "json_v2_ingest": jleg, "store_get_dependencies": sleg,
                        "mysql_rows": rows_leg, "put_trace_loop": ptl, "put_trace_loop_c4": ptc4, "c5": c5},

@@ -36,12 +36,13 @@
 extern "C" {
 #endif
 
-#define ZDL_ABI_VERSION 6  /* 2: zdl_config.n_devices / device_ids, RCCL combine; 3: zdl_kernel_times
+#define ZDL_ABI_VERSION 7  /* 2: zdl_config.n_devices / device_ids, RCCL combine; 3: zdl_kernel_times
                               per phase of a put (mid_ms, giant_ms, sparse_ms); 4: trace id widths
                               (zdl_store_append_ids, zdl_decoded.dev_trace_wide); 5: zdl_put_trace,
                               a trace whose Trace.merge throws adds nothing, a started link locks
                               the context until zdl_link_finish; 6: zdl_comm_init_local (a job of
-                              contexts of one process), a sparse job sums by reduce-scatter */
+                              contexts of one process), a sparse job sums by reduce-scatter; 7: zdl_kernel_times
+                              log_entries / sparse_entries (the reduce's and the merge's inputs) */
 
 /* ---- status codes ---- */
 #define ZDL_OK          0
@@ -171,6 +172,9 @@ typedef struct zdl_kernel_times {  /* the last put's phases (ZDL_FLAG_TIMING_ALL
   float mid_ms;      /* k_mid: traces of 65..192 spans, one wave each */
   float giant_ms;    /* the device-wide big-trace tier (sparse contexts), host syncs included */
   float sparse_ms;   /* sparse contexts: gathering, sorting and merging the put's link log */
+  uint64_t log_entries;     /* LOG mode: the entries k_link logged for the reduce (the hot corner's
+                               links not included) */
+  uint64_t sparse_entries;  /* sparse contexts: the link-log entries the merge sorted */
 } zdl_kernel_times;
 
 /* Context lifecycle. zdl_create returns NULL on failure (zdl_create_error() says why). */

@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version():
     from zipkin_amd import _native
-    assert _native.lib().zdl_abi_version() == _native.ZDL_ABI_VERSION == 6
+    assert _native.lib().zdl_abi_version() == _native.ZDL_ABI_VERSION == 7
 
 
 def test_create_rejects_bad_config_without_device():

@@ -52,7 +52,7 @@ EXPORTS = (
     "zdl_tree_export", "zdl_tree_reasons", "zdl_decode_json_v2", "zdl_decode_retry", "zdl_decoder_struct_ms", "zdl_decoder_exact_spans",
     "zdl_link_start", "zdl_link_finish", "zdl_put_trace", "zdl_comm_init_local",
 )
-ZDL_ABI_VERSION = 6
+ZDL_ABI_VERSION = 7
 ZDL_COMM_ID_BYTES = 128
 
 
@@ -100,7 +100,8 @@ class KernelTimes(C.Structure):
     _fields_ = [("plan_ms", C.c_float), ("tiles_ms", C.c_float), ("big_ms", C.c_float),
                 ("reduce_ms", C.c_float), ("compact_ms", C.c_float), ("n_tiles", C.c_uint32),
                 ("n_big", C.c_uint32), ("grid", C.c_uint32), ("full_ms", C.c_float), ("mid_ms", C.c_float),
-                ("giant_ms", C.c_float), ("sparse_ms", C.c_float)]
+                ("giant_ms", C.c_float), ("sparse_ms", C.c_float), ("log_entries", C.c_uint64),
+                ("sparse_entries", C.c_uint64)]
 
 
 class ZdlError(RuntimeError):

@@ -1771,6 +1771,8 @@ struct zdl_ctx {
   uint32_t lk_n = 0;
   uint32_t lk_stride = 1, lk_puts = 0;  // time every lk_stride-th put
   zdl_kernel_times times = {};
+  uint32_t last_log_lP = 0;    // the last put's LOG partitions (0: not LOG mode), for log_entries
+  uint64_t last_sparse_E = 0;  // the last put's sparse link-log entries
   // a lazy put (Args::lazy): launched k_link only; k_mid / k_tail follow only if its flag says
   // so (resolve_lazy), with the put's arguments kept here
   bool lazy_pending = false;
@@ -1855,6 +1857,15 @@ void put_times(zdl_ctx* c) {
   c->times.giant_ms = ev_ms(c, 3, 8);
   c->times.big_ms = ev_ms(c, 8, 4);
   c->times.sparse_ms = ev_ms(c, 4, 9);
+  c->times.sparse_entries = c->last_sparse_E;
+  c->times.log_entries = 0;
+  if (c->last_log_lP) {  // k_pbase's total (the put's work is complete here)
+    uint32_t v = 0;
+    if (hipMemcpyAsync(&v, c->lg_tot.p + PMAX + c->last_log_lP, 4, hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
+        hipStreamSynchronize(c->stream) == hipSuccess)
+      c->times.log_entries = v;
+    (void)hipGetLastError();
+  }
 }
 
 }  // namespace
@@ -2001,8 +2012,8 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
   if (e == hipSuccess) {
     const char* pe = getenv("ZDL_PROF");
     c->prof_on = pe && pe[0] == '1';
-    if (c->prof_on) {  // 12 phase counters, then (start, end) wall clock of every k_link wave
-      const size_t words = 12 + 2 * (size_t)c->cus * lk::wgs_per_cu * lk::waves(0);
+    if (c->prof_on) {  // 12 phase counters, then (start, end, hardware id) of every k_link wave
+      const size_t words = 12 + 3 * (size_t)c->cus * lk::wgs_per_cu * lk::waves(0);
       e = c->prof.ensure(words);
       if (e == hipSuccess) e = hipMemsetAsync(c->prof.p, 0, words * 8, c->stream);
     }
@@ -2072,16 +2083,22 @@ void zdl_destroy(zdl_ctx* c) {
     }
     // the last put's k_link waves: when each finished after the first one started (100 MHz clock)
     const size_t W = (size_t)c->cus * lk::wgs_per_cu * lk::waves(0);
-    std::vector<unsigned long long> w(2 * W);
-    if (hipMemcpy(w.data(), c->prof.p + 12, 2 * W * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+    std::vector<unsigned long long> w(3 * W);
+    if (hipMemcpy(w.data(), c->prof.p + 12, 3 * W * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+      if (const char* dp = getenv("ZDL_PROF_DUMP")) {  // (start, end, hardware id) per wave, raw u64
+        if (FILE* f = fopen(dp, "wb")) {
+          fwrite(w.data(), 8, w.size(), f);
+          fclose(f);
+        }
+      }
       unsigned long long t0 = ~0ull;
       for (size_t i = 0; i < W; ++i)
-        if (w[2 * i]) t0 = std::min(t0, w[2 * i]);
+        if (w[3 * i]) t0 = std::min(t0, w[3 * i]);
       std::vector<double> end, busy;
       for (size_t i = 0; i < W; ++i)
-        if (w[2 * i] && w[2 * i + 1]) {
-          end.push_back((double)(w[2 * i + 1] - t0) * 0.01);
-          busy.push_back((double)(w[2 * i + 1] - w[2 * i]) * 0.01);
+        if (w[3 * i] && w[3 * i + 1]) {
+          end.push_back((double)(w[3 * i + 1] - t0) * 0.01);
+          busy.push_back((double)(w[3 * i + 1] - w[3 * i]) * 0.01);
         }
       std::sort(end.begin(), end.end());
       std::sort(busy.begin(), busy.end());
@@ -2345,6 +2362,7 @@ static int sparse_finish(zdl_ctx* c, uint32_t ep, uint32_t lW, uint64_t n_spans,
   HIP_TRY(c, hipStreamSynchronize(s));
   const uint64_t E = (uint64_t)((uint32_t*)c->h_meta)[0] + ((uint32_t*)c->h_meta)[1];
   if (E > 4 * n_spans) return fail(c, ZDL_EDEVICE, "sparse: more links than the log holds");
+  c->last_sparse_E = E;
   if (E == 0) return ZDL_OK;
   HIP_TRY(c, c->lin.ensure(E));
   hipLaunchKernelGGL(k_seg_copy, dim3((unsigned)((E + SEG_TILE - 1) / SEG_TILE)), dim3(256), 0, s, c->lg.p,
@@ -2747,6 +2765,8 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
                                               lmode),
                              c->stream));
   ev_record(c, 7);
+  c->last_log_lP = tm == TM_LOG ? lP : 0u;
+  c->last_sparse_E = 0;
   if (tm == TM_LOG) {  // group the log by partition, count each partition in LDS (zdl_log.inc)
 #if ZDL_LOG_ROWS
     // rows = k_link's workgroups (the column prefix over 512 rows), a scatter workgroup per row
