@@ -1705,6 +1705,13 @@ struct zdl_ctx {
   DevBuf<uint8_t> gg_stat;
   GArgs gg_args{};            // the tier's arguments, from giant_prep to giant_run
   hipEvent_t gg_ev = nullptr;  // k_g_prep's totals copied to h_gmeta
+  // ZDL_BIG_SIDE=1: k_big beside k_mid and the giant tier on a stream of its own, joined before
+  // k_tail. Measured at C5 (8 HW queues, bit-exact): one put alone 6.68 -> 6.49 ms, two contexts
+  // in flight 4.74 -> 4.97 ms (the kernels share the CUs, k_big<1024>'s 150 KB of LDS keeps the
+  // tier's workgroups off its CU, and a third and fourth stream share the hardware queues). Off.
+  hipStream_t side = nullptr;
+  hipEvent_t side_ev = nullptr;
+  bool big_side = false;
   uint64_t gg_ntmax = 0;
   uint32_t* h_gmeta = nullptr;  // pinned: the tier's GM_* words
   int big_exact = 0;
@@ -2021,6 +2028,8 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
     c->skip = sk ? (uint32_t)strtoul(sk, nullptr, 0) : 0u;
     const char* be = getenv("ZDL_BIG_EXACT");
     c->big_exact = be && be[0] == '1';
+    const char* bs = getenv("ZDL_BIG_SIDE");
+    c->big_side = bs && bs[0] == '1';
     const char* wb = getenv("ZDL_WAVE_BIG");
     c->wave_big = !(wb && wb[0] == '0');
     const char* gm = getenv("ZDL_GIANT_MIN");
@@ -2129,6 +2138,8 @@ void zdl_destroy(zdl_ctx* c) {
   c->gg_part32.release();
   c->gg_part64.release();
   if (c->gg_ev) (void)hipEventDestroy(c->gg_ev);
+  if (c->side_ev) (void)hipEventDestroy(c->side_ev);
+  if (c->side) (void)hipStreamDestroy(c->side);
   c->gg_base.release(); c->gg_h0.release(); c->gg_root.release(); c->gg_tsroot.release(); c->gg_tsmin.release();
   c->gg_rootidx.release(); c->gg_stat.release();
   if (c->h_gmeta) (void)hipHostFree(c->h_gmeta);
@@ -2439,6 +2450,34 @@ static int giant_prep(zdl_ctx* c, Args& A, uint64_t n_spans, uint64_t n_traces) 
   HIP_TRY(c, hipMemcpyAsync(c->h_gmeta, c->gg_meta.p, GM_WORDS * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(c, hipEventRecord(c->gg_ev, s));
   c->gg_ntmax = ntmax;
+  // every back-list entry has its verdict (giant or not) and the rest list is final: k_big and
+  // k_tail take the rest list (k_g_par hands the traces the join rejects to k_tail's exact list
+  // itself), so k_big need not wait for the tier
+  A.gstat = c->gg_stat.p;
+  A.grest = c->gg_rest.p;
+  A.grest_n = c->gg_meta.p + GM_REST;
+  return ZDL_OK;
+}
+
+// k_big<256> and k_big<1024> on the context's side stream, behind k_g_prep (gg_ev): the back
+// list's non-giant traces, one workgroup each - latency-bound work that runs beside k_mid and the
+// giant tier instead of after them (their scratch is disjoint: every array is indexed by span
+// position at the same scale, zdl_giant.inc). side_ev joins the main stream before k_tail.
+static int launch_big_side(zdl_ctx* c, Args& A, int wmode) {
+  if (!c->side) HIP_TRY(c, hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+  if (!c->side_ev) HIP_TRY(c, hipEventCreateWithFlags(&c->side_ev, hipEventDisableTiming));
+  HIP_TRY(c, hipStreamWaitEvent(c->side, c->gg_ev, 0));
+  void* kargs[] = {&A};
+  hipError_t be = hipLaunchKernel((const void*)k_big<256>, dim3((unsigned)c->cus * 4), dim3(256), kargs,
+                                  (size_t)KB_SMALL_LDS, c->side);
+  if (be == hipSuccess)
+    be = hipLaunchKernel((const void*)k_big<TAIL_WG>, dim3(c->grid), dim3(TAIL_WG), kargs, tail_block_bytes(wmode),
+                         c->side);
+  if (be == hipSuccess) be = hipEventRecord(c->side_ev, c->side);
+  if (be != hipSuccess) {
+    c->poisoned = true;
+    return hip_fail(c, be, "k_big launch (side stream)");
+  }
   return ZDL_OK;
 }
 
@@ -2447,10 +2486,7 @@ static int giant_run(zdl_ctx* c, Args& A) {
   HIP_TRY(c, hipEventSynchronize(c->gg_ev));  // k_link and k_g_prep (k_mid may still run)
   GArgs& G = c->gg_args;
   const uint32_t ng = c->h_gmeta[GM_G], nt = c->h_gmeta[GM_NT], maxn = c->h_gmeta[GM_MAXN], nh = c->h_gmeta[GM_NH];
-  if (ng == 0) return ZDL_OK;  // k_tail takes the whole back list as usual
-  A.gstat = c->gg_stat.p;  // every back-list entry has its verdict now
-  A.grest = c->gg_rest.p;  // k_tail links the rest list only (k_g_par appends rejected giants)
-  A.grest_n = c->gg_meta.p + GM_REST;
+  if (ng == 0) return ZDL_OK;  // the rest list is the whole back list
   if (nt > c->gg_ntmax || maxn > (uint32_t)GMAXN || nh == 0xFFFFFFFFu)
     return fail(c, ZDL_EDEVICE, "giant tier: inconsistent sizes");
   HIP_TRY(c, c->gg_H.ensure(nh));
@@ -2807,11 +2843,17 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
     return ZDL_OK;
   }
   const bool giant = c->sparse && c->giant_min > 0 && !c->ord && !c->days;
+  bool big_side = false;
   if (giant) {  // the giant tier's split of the back list, before k_mid (giant_prep)
     const int grc = giant_prep(c, A, n_spans, n_traces);
     if (grc != ZDL_OK) {
       c->poisoned = true;  // k_link ran: the counter slots hold this put's counts
       return grc;
+    }
+    if (A.bstat && c->big_side) {
+      const int brc = launch_big_side(c, A, wmode);
+      if (brc != ZDL_OK) return brc;
+      big_side = true;
     }
   }
   if (A.wb_max) {  // big_list's front (WSMALL < n <= WB_MAX spans): one wave per trace
@@ -2831,7 +2873,13 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
     }
   }
   ev_record(c, 8);
-  if (A.bstat) {
+  if (big_side) {
+    const hipError_t we = hipStreamWaitEvent(c->stream, c->side_ev, 0);
+    if (we != hipSuccess) {
+      c->poisoned = true;
+      return hip_fail(c, we, "join the side stream");
+    }
+  } else if (A.bstat) {
     const int brc = launch_big(c, kargs, wmode);
     if (brc != ZDL_OK) return brc;
   }
