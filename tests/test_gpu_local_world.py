@@ -140,6 +140,42 @@ def test_insertion_order_across_ranks(W, config):
         assert got[k] == exp
 
 
+@pytest.mark.parametrize("W", [3, 8])
+def test_insertion_order_local_order_tags(W, monkeypatch):
+    """The combine's second tagging (beyond 64 ranks: each rank's first ranks replaced by their
+    order among its own pairs, rank << 32 | index), forced at a small world: the same order."""
+    monkeypatch.setenv("ZDL_ORD_LOCAL_ORDER", "1")
+    w = synth.C4.scaled(20_000)
+    cols = synth.generate(w)
+    parts = [_empty()] + shard.partition_columns(cols, W - 1)
+    ctxs = _job(parts, w.total_services, insertion_order=True, puts=2)
+    try:
+        got = _concurrently(ctxs, lambda k, c: _tuples(*c.link(N.ZDL_ORDER_INSERTION)))
+    finally:
+        _close(ctxs)
+    exp = _merge_in_rank_order(parts)
+    assert len(exp) > 100
+    for k in range(W):
+        assert [(a, b, n // 2, e // 2) for a, b, n, e in got[k]] == exp
+
+
+def test_insertion_order_beyond_64_ranks():
+    """66 ranks (the rank tag's 6 bits no longer suffice): the local-order tags, exact order."""
+    W = 66
+    w = synth.C2.scaled(6_600)
+    cols = synth.generate(w)
+    parts = shard.partition_columns(cols, W)
+    ctxs = _job(parts, w.total_services, insertion_order=True)
+    try:
+        got = _concurrently(ctxs, lambda k, c: _tuples(*c.link(N.ZDL_ORDER_INSERTION)))
+    finally:
+        _close(ctxs)
+    exp = _merge_in_rank_order(parts)
+    assert len(exp) > 100
+    for k in (0, 1, 33, W - 1):
+        assert got[k] == exp
+
+
 def test_insertion_order_empty_first_rank():
     """Rank 0 holds nothing: its tags never win the MIN; the order starts at rank 1's list."""
     w = synth.C4.scaled(20_000)

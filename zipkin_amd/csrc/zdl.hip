@@ -1678,6 +1678,9 @@ struct zdl_ctx {
   SparseTable gslice;                // sparse combine: this rank's cell range of the job's list
   DevBuf<unsigned long long> red_call, red_err;  // the summed tables
   DevBuf<unsigned long long> red_first;          // insertion order: the job's first ranks (MIN)
+  DevBuf<unsigned long long> ord_lk;             // (the local-order combine: sorted first ranks,
+  DevBuf<uint32_t> ord_lv, ord_lv2;              //  their cells before and after the sort,
+  DevBuf<unsigned char> ord_ltmp;                //  the sort's scratch)
   // sparse combine (device groups / jobs above 1024 services): every device's or rank's sorted
   // list gathered here (cell, call, err), summed into gacc (sparse_add: DependencyLinker.merge)
   DevBuf<uint32_t> gx_cell;
@@ -1696,6 +1699,8 @@ struct zdl_ctx {
   // the device-wide big-trace tier (zdl_giant.inc, sparse contexts): per-put lists and scratch
   int giant_min = 2048;  // traces longer than this (ZDL_GIANT_MIN; 0: off, k_tail's workgroups)
   DevBuf<uint32_t> gg_bi, gg_n, gg_tile0, gg_bad, gg_tile_g, gg_bstart, gg_blen, gg_meta, gg_H, gg_rest;
+  DevBuf<unsigned long long> gg_jl0, gg_jl1;  // k_g_jump's live lists
+  DevBuf<uint32_t> gg_jc;                     // and their segments' lengths
   DevBuf<unsigned char> gg_tmp;
   DevBuf<uint32_t> gg_part32;  // k_g_prep_*'s block sums, then carries
   DevBuf<unsigned long long> gg_part64;
@@ -2071,6 +2076,7 @@ void zdl_destroy(zdl_ctx* c) {
   c->red_call.release();
   c->red_err.release();
   c->red_first.release();
+  c->ord_lk.release(); c->ord_lv.release(); c->ord_lv2.release(); c->ord_ltmp.release();
   for (auto& x : c->xs) x.release();
   c->gslice.release();
   (void)hipSetDevice(c->device);
@@ -2134,6 +2140,9 @@ void zdl_destroy(zdl_ctx* c) {
   for (auto* b : {&c->gg_bi, &c->gg_n, &c->gg_tile0, &c->gg_bad, &c->gg_tile_g, &c->gg_bstart, &c->gg_blen,
                   &c->gg_meta, &c->gg_H, &c->gg_rest})
     b->release();
+  c->gg_jl0.release();
+  c->gg_jl1.release();
+  c->gg_jc.release();
   c->gg_tmp.release();
   c->gg_part32.release();
   c->gg_part64.release();
@@ -2491,6 +2500,15 @@ static int giant_run(zdl_ctx* c, Args& A) {
     return fail(c, ZDL_EDEVICE, "giant tier: inconsistent sizes");
   HIP_TRY(c, c->gg_H.ensure(nh));
   G.H = c->gg_H.p;
+  const uint32_t jgrid = std::min<uint32_t>(8 * ((nt + 7) / 8), (uint32_t)c->cus * 2);  // k_g_jump's grid
+  const size_t jcap = (size_t)((8 * ((nt + 7) / 8) + jgrid - 1) / jgrid) * GT;           // (g_jump_cap)
+  HIP_TRY(c, c->gg_jl0.ensure(jcap * jgrid));  // a block's segment holds its round-0 spans
+  HIP_TRY(c, c->gg_jl1.ensure(jcap * jgrid));
+  HIP_TRY(c, c->gg_jc.ensure(2 * (size_t)jgrid));
+  G.jl[0] = c->gg_jl0.p;
+  G.jl[1] = c->gg_jl1.p;
+  G.jc[0] = c->gg_jc.p;
+  G.jc[1] = c->gg_jc.p + jgrid;
   G.nt = nt;
   G.per = (nt + 7) / 8;
   const dim3 tg(8 * G.per), tb(GT);
@@ -2503,7 +2521,7 @@ static int giant_run(zdl_ctx* c, Args& A) {
   // depth (<= n); rounds after convergence return at once (the flag)
   int rounds = 1;
   for (uint64_t reach = 3; reach < (uint64_t)maxn && rounds < GROUNDS_MAX; reach *= 3) ++rounds;
-  const dim3 jg(std::min<uint32_t>(8 * G.per, (uint32_t)c->cus * 2));  // persistent; a multiple of 8
+  const dim3 jg(jgrid);  // persistent; a multiple of 8 (8 * G.per = 8 * ceil(nt / 8))
   for (int r = 0; r < rounds; ++r) hipLaunchKernelGGL(k_g_jump, jg, tb, 0, s, A, G, r);
   hipLaunchKernelGGL(k_g_rules, tg, tb, 0, s, A, G);
   HIP_TRY(c, hipGetLastError());
@@ -4577,18 +4595,53 @@ __global__ void k_ord_tag(const unsigned long long* __restrict__ first, unsigned
     out[i] = zdl_xplan::ord_tag(first[i], rank);
 }
 
+__global__ void k_iota32(uint32_t* __restrict__ v, uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    v[i] = (uint32_t)i;
+}
+// The local-order tags: the cell at sorted position j (its rank's j-th first-seen pair) gets
+// rank << 32 | j; a pair the rank never saw stays ~0
+__global__ void k_ord_local(const unsigned long long* __restrict__ key, const uint32_t* __restrict__ cell,
+                            unsigned long long* __restrict__ out, uint64_t n, int rank) {
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x)
+    out[cell[j]] = key[j] == ~0ull ? ~0ull : (((unsigned long long)(uint32_t)rank << 32) | j);
+}
+
 // Insertion order across a job (zdl_xplan.h): the sums as comm_sum_tables, and one MIN of the
 // rank-tagged first ranks, so a pair sits where DependencyLinker.merge over the ranks' link()
-// lists, concatenated in rank order, first sees it (DependencyLinker.java:189-204).
+// lists, concatenated in rank order, first sees it (DependencyLinker.java:189-204). Only the order
+// of the tags matters (link_insertion sorts by them), so beyond 64 ranks each rank replaces its
+// first ranks by their order among its own pairs (a local sort of its S x S cells) and tags that
+// index with its rank in the upper 32 bits: any world size, no limit on the spans put.
 static int comm_sum_ord(zdl_ctx* c) {
-  if (c->span_base >= zdl_xplan::ORD_POS_LIMIT)
-    return fail(c, ZDL_EINVAL, "insertion order across ranks: more than 2^34 spans put on this rank");
   const size_t SS = (size_t)c->rows * c->S;
   HIP_TRY(c, c->red_call.ensure(SS));
   HIP_TRY(c, c->red_err.ensure(SS));
   HIP_TRY(c, c->red_first.ensure(SS));
-  hipLaunchKernelGGL(k_ord_tag, dim3((unsigned)std::min<size_t>((SS + 255) / 256, 4096)), dim3(256), 0, c->stream,
-                     c->first.p, c->red_first.p, (uint64_t)SS, c->comm_rank);
+  const int world = c->comm_world;
+  const char* lo = getenv("ZDL_ORD_LOCAL_ORDER");  // (tests: the local-order tags at any size)
+  const unsigned g = (unsigned)std::min<size_t>((SS + 255) / 256, 4096);
+  // (the choice is the job's: every rank sees the same world size)
+  if (world > zdl_xplan::ORD_MAX_WORLD || (lo && lo[0] == '1')) {
+    if (SS >= (1ull << 32)) return fail(c, ZDL_EINVAL, "insertion order across ranks: a table of 2^32 cells or more");
+    HIP_TRY(c, c->ord_lk.ensure(SS));
+    HIP_TRY(c, c->ord_lv.ensure(SS));
+    HIP_TRY(c, c->ord_lv2.ensure(SS));
+    hipLaunchKernelGGL(k_iota32, dim3(g), dim3(256), 0, c->stream, c->ord_lv.p, (uint64_t)SS);
+    size_t tb = 0;
+    HIP_TRY(c, hipcub::DeviceRadixSort::SortPairs(nullptr, tb, c->first.p, c->ord_lk.p, c->ord_lv.p, c->ord_lv2.p,
+                                                   (int)SS, 0, 64, c->stream));
+    HIP_TRY(c, c->ord_ltmp.ensure(tb));
+    HIP_TRY(c, hipcub::DeviceRadixSort::SortPairs(c->ord_ltmp.p, tb, c->first.p, c->ord_lk.p, c->ord_lv.p,
+                                                   c->ord_lv2.p, (int)SS, 0, 64, c->stream));
+    hipLaunchKernelGGL(k_ord_local, dim3(g), dim3(256), 0, c->stream, c->ord_lk.p, c->ord_lv2.p, c->red_first.p,
+                       (uint64_t)SS, c->comm_rank);
+  } else {
+    if (c->span_base >= zdl_xplan::ORD_POS_LIMIT)
+      return fail(c, ZDL_EINVAL, "insertion order across ranks: more than 2^34 spans put on this rank");
+    hipLaunchKernelGGL(k_ord_tag, dim3(g), dim3(256), 0, c->stream, c->first.p, c->red_first.p, (uint64_t)SS,
+                       c->comm_rank);
+  }
   HIP_TRY(c, hipGetLastError());
   const XRed ops[3] = {{c->call.p, c->red_call.p, SS, 0}, {c->errc.p, c->red_err.p, SS, 0},
                        {c->red_first.p, c->red_first.p, SS, 1}};
@@ -4736,8 +4789,6 @@ int zdl_comm_init(zdl_ctx* c, const uint8_t* id, int rank, int world) {
   if (const int frc = stage_flush(c)) return frc;  // staged putTrace calls come first
   if (!c->sub.empty()) return fail(c, ZDL_EINVAL, "zdl_comm_init: a device group has its own communicator");
   if (c->days) return fail(c, ZDL_EINVAL, "zdl_comm_init: daily buckets are per process");
-  if (c->ord && world > zdl_xplan::ORD_MAX_WORLD)
-    return fail(c, ZDL_EINVAL, "zdl_comm_init: insertion order across at most 64 ranks");
   if (in_job(c)) return fail(c, ZDL_EINVAL, "zdl_comm_init: already joined");
   if (c->sparse && world > zdl_xplan::MAX_WORLD) return fail(c, ZDL_EINVAL, "zdl_comm_init: a sparse job has at most 1024 ranks");
   HIP_TRY(c, enter(c));
@@ -4765,8 +4816,6 @@ int zdl_comm_init_local(zdl_ctx* const* ctxs, int world) {
     if (!c->sub.empty()) return fail(c, ZDL_EINVAL, "zdl_comm_init_local: a device group has its own communicator");
     if (c->days) return fail(c, ZDL_EINVAL, "zdl_comm_init_local: daily buckets are per process");
     if (in_job(c)) return fail(c, ZDL_EINVAL, "zdl_comm_init_local: already joined");
-    if (c->ord && world > zdl_xplan::ORD_MAX_WORLD)
-      return fail(c, ZDL_EINVAL, "zdl_comm_init_local: insertion order across at most 64 ranks");
     const zdl_ctx* c0 = ctxs[0];
     if (c->device != c0->device || c->S != c0->S || c->rows != c0->rows || c->sparse != c0->sparse || c->ord != c0->ord)
       return fail(c, ZDL_EINVAL, "zdl_comm_init_local: the ranks need one device, one service count and one mode");
