@@ -1999,7 +1999,7 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
       e = hipFuncSetAttribute(k_link_fn(tm, w), hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)link_block_bytes(w, tm));
     for (int m = 1; m <= 5 && e == hipSuccess; ++m)
-      for (int tm = 0; tm < (m == 5 ? 4 : m == 4 ? 3 : 2) && e == hipSuccess; ++tm)
+      for (int tm = 0; tm < (m == 5 ? 4 : (m == 4 || m == 2) ? 3 : 2) && e == hipSuccess; ++tm)
         e = hipFuncSetAttribute(k_link_fn(tm, w, m), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)link_block_bytes(m == 3 ? 0 : w, tm, m));
   }
