@@ -316,6 +316,42 @@ def put_trace_c4_leg(device, traces=1_000_000, reps=3):
                     "the CPU figure is one linker on one thread over the same traces"}
 
 
+def facade_put_trace_leg(device, traces=20_000):
+    """The shipped Python facade's call pattern: zipkin_amd.linker.DependencyLinker.put_trace once
+    per trace, each a list of zipkin2 Span objects (C2's first `traces` traces converted, not
+    timed), then link() (insertion order, DependencyLink objects). The time is Python's: every
+    span's fields are read and packed into columns on the host before the engine sees them (the
+    JNI caller passes columns; put_trace_loop times that path). Links compared by service name with
+    the C++ restatement over the same traces."""
+    from oracle import ref
+    from zipkin_amd import synth
+    from zipkin_amd.linker import DependencyLinker
+    w = synth.C2.scaled(traces)
+    cols = synth.generate(w)
+    trs = synth.spans_of(cols, w, traces)
+    lk = DependencyLinker(device=device)
+    warm = 200  # (the engine context and the dictionaries exist before the timed calls)
+    for tr in trs[:warm]:
+        lk.put_trace(tr)
+    lk.link()
+    t0 = time.perf_counter()
+    for tr in trs[warm:]:
+        lk.put_trace(tr)
+    links = lk.link()
+    t = time.perf_counter() - t0
+    timed = len(trs) - warm
+    names = synth.service_names(w)
+    st, p, c, n, e = ref.link(cols, threads=4)
+    exp = sorted(zip([names[i] for i in p], [names[i] for i in c], n.tolist(), e.tolist()))
+    got = sorted((l.parent, l.child, l.call_count, l.error_count) for l in links)
+    timed_spans = int(cols.offsets[-1] - cols.offsets[warm])
+    return {"traces": timed, "spans": timed_spans, "ms": t * 1e3, "us_per_call": t / timed * 1e6,
+            "spans_per_s": timed_spans / t, "parity": "same links" if st == 0 and got == exp else "MISMATCH",
+            "note": "DependencyLinker.put_trace per trace from Python (Span objects, host packing in Python) + "
+                    "link(); C2's first traces; the Python work dominates - the native per-trace path is "
+                    "put_trace_loop"}
+
+
 def _sorted_links(p, c, n, e):
     o = np.lexsort((c, p))
     return p[o], c[o], n[o], e[o]
@@ -901,6 +937,11 @@ def main():
         log(f"putTrace loop c4: {ptc4['ms']:.1f} ms for {ptc4['traces']} calls ({ptc4['merge_run_traces']} with merge "
             f"runs), {ptc4['us_per_call']:.3f} us/call; one C++ linker on 1 thread {ptc4['cpu_single_thread_ms']:.0f} "
             f"ms ({ptc4['speedup_vs_single_thread']:.1f}x), links {ptc4['parity']}")
+    fpt = None
+    if side and not args.no_put_trace:
+        fpt = facade_put_trace_leg(local)
+        log(f"putTrace from the Python facade: {fpt['ms']:.0f} ms for {fpt['traces']} calls "
+            f"({fpt['us_per_call']:.1f} us/call, {fpt['spans_per_s']:.3e} spans/s), links {fpt['parity']}")
     c5 = None
     if side and not args.no_c5:
         c5 = c5_leg(local, parity=not args.no_parity, threads=cpu_info()["usable"], host_threads=args.c5_host_threads)
@@ -984,7 +1025,8 @@ def main():
                        "log_reduce": log_reduce,
                        "parity": parity, "links": int(len(p)), "insertion_order": ins, "host_buffers": h2d,
                        "proto3_ingest": p3, "json_v2_ingest": jleg, "store_get_dependencies": sleg,
-                       "mysql_rows": rows_leg, "put_trace_loop": ptl, "put_trace_loop_c4": ptc4, "c5": c5},
+                       "mysql_rows": rows_leg, "put_trace_loop": ptl, "put_trace_loop_c4": ptc4, "facade_put_trace_python": fpt,
+                       "c5": c5},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "k_link", "algorithmic_bytes_per_launch": klink_bytes,

@@ -101,33 +101,34 @@ def port_flags_of(s: Span) -> int:
 
 def pack_traces(traces: Sequence[Sequence[Span]], svc: Dictionary, ip4: Dictionary,
                 ip6: Dictionary) -> Columns:
-    n = sum(len(t) for t in traces)
-    tl = np.empty(n, np.uint64)
-    ids = np.empty(n, np.uint64)
-    pids = np.empty(n, np.uint64)
-    ls = np.empty(n, np.int32)
-    rs = np.empty(n, np.int32)
-    l4 = np.empty(n, np.int32)
-    l6 = np.empty(n, np.int32)
-    pf = np.empty(n, np.uint32)
-    ts = np.empty(n, np.int64)
-    off = np.zeros(len(traces) + 1, np.uint64)
-    i = 0
-    for t, trace in enumerate(traces):
+    """The columns of `traces` (putTrace calls' spans, in call order). One pass of Python over the
+    spans into lists, then one conversion per column (element-wise stores into numpy arrays cost
+    more than the spans' own attribute reads)."""
+    tl, ids, pids, ls, rs, l4, l6, pf, ts = [], [], [], [], [], [], [], [], []
+    off = [0]
+    sid, i4, i6 = svc.id, ip4.id, ip6.id
+    for trace in traces:
         for s in trace:
-            tl[i] = int(s.trace_lo, 16)
-            ids[i] = int(s.id, 16)
-            pids[i] = int(s.parent_id, 16) if s.parent_id is not None else 0
+            tl.append(int(s.trace_lo, 16))
+            ids.append(int(s.id, 16))
+            pids.append(int(s.parent_id, 16) if s.parent_id is not None else 0)
             le = s.local_endpoint
-            ls[i] = svc.id(le.service_name) if le else -1
-            l4[i] = ip4.id(le.ipv4) if le else -1
-            l6[i] = ip6.id(le.ipv6) if le else -1
-            rs[i] = svc.id(s.remote_endpoint.service_name) if s.remote_endpoint else -1
-            pf[i] = port_flags_of(s)
-            ts[i] = s.timestamp
-            i += 1
-        off[t + 1] = i
-    return Columns(tl, ids, pids, ls, rs, l4, l6, pf, ts, off)
+            if le is not None:
+                ls.append(sid(le.service_name))
+                l4.append(i4(le.ipv4))
+                l6.append(i6(le.ipv6))
+            else:
+                ls.append(-1)
+                l4.append(-1)
+                l6.append(-1)
+            re = s.remote_endpoint
+            rs.append(sid(re.service_name) if re is not None else -1)
+            pf.append(port_flags_of(s))
+            ts.append(s.timestamp)
+        off.append(len(ids))
+    return Columns(np.array(tl, np.uint64), np.array(ids, np.uint64), np.array(pids, np.uint64),
+                   np.array(ls, np.int32), np.array(rs, np.int32), np.array(l4, np.int32), np.array(l6, np.int32),
+                   np.array(pf, np.uint32), np.array(ts, np.int64), np.array(off, np.uint64))
 
 
 def concat_columns(parts: Iterable[Columns]) -> Columns:

@@ -14,6 +14,8 @@ from typing import Optional
 import numpy as np
 
 from .columnar import Columns
+from ._native import PF_ERROR as _PF_ERROR, PF_KIND_SHIFT as _PF_KIND_SHIFT, PF_RIP4 as _PF_RIP4, PF_RIP6 as _PF_RIP6
+from ._native import PF_RPORT as _PF_RPORT, PF_SHARED_SHIFT as _PF_SHARED_SHIFT
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SYNTH_PATH = os.path.join(HERE, "libzdl_synth.so")
@@ -188,3 +190,38 @@ def put_trace_loop(ctx, cols: Columns, timestamps: bool = False) -> None:
     rc = L.zdl_synth_put_trace_loop(fn, ctx.h, C.byref(sc), cols.offsets.ctypes.data, cols.n_traces, C.byref(at))
     if rc != 0:
         ctx.check(rc)
+
+
+def spans_of(cols: Columns, w: "Workload", n_traces: int):
+    """The first n_traces traces of `cols` as zipkin2 Span objects (one list per trace), for
+    timing the Python facade's putTrace path: service ids become service_names(w), local ip ids
+    dotted quads / v6 literals, a remote endpoint's flagged ip or port a fixed value (the linker
+    reads only their presence)."""
+    from .model import Endpoint, Kind, Span
+    names = service_names(w)
+    kinds = {0: Kind.CLIENT, 1: Kind.SERVER, 2: Kind.PRODUCER, 3: Kind.CONSUMER}
+    off = cols.offsets
+    out = []
+    for t in range(min(n_traces, cols.n_traces)):
+        tr = []
+        for i in range(int(off[t]), int(off[t + 1])):
+            pf = int(cols.port_flags[i])
+            ls, rs = int(cols.local_svc[i]), int(cols.remote_svc[i])
+            l4, l6 = int(cols.local_ip4[i]), int(cols.local_ip6[i])
+            le = None
+            if ls >= 0 or l4 >= 0 or l6 >= 0 or (pf & 0xFFFF):
+                le = Endpoint(names[ls] if ls >= 0 else None,
+                              f"10.{(l4 >> 16) & 255}.{(l4 >> 8) & 255}.{l4 & 255}" if l4 >= 0 else None,
+                              f"2001:db8::{l6:x}" if l6 >= 0 else None, pf & 0xFFFF)
+            re = None
+            if rs >= 0 or pf & (_PF_RIP4 | _PF_RIP6 | _PF_RPORT):
+                re = Endpoint(names[rs] if rs >= 0 else None, "10.9.9.9" if pf & _PF_RIP4 else None,
+                              "2001:db8::99" if pf & _PF_RIP6 else None, 9000 if pf & _PF_RPORT else 0)
+            sh = (pf >> _PF_SHARED_SHIFT) & 3
+            pid = int(cols.parent_id[i])
+            tr.append(Span(f"{int(cols.trace_lo[i]):016x}", f"{int(cols.id[i]):016x}",
+                           f"{pid:016x}" if pid else None, kinds.get((pf >> _PF_KIND_SHIFT) & 7),
+                           None, int(cols.timestamp[i]), 0, le, re, (),
+                           (("error", ""),) if pf & _PF_ERROR else (), None if sh == 0 else sh == 2, None))
+        out.append(tr)
+    return out
