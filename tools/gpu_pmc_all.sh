@@ -3,7 +3,7 @@
 # command one rocprofv3 --kernel-trace --stats run (durations) and two PMC runs (FETCH_SIZE,
 # WRITE_SIZE), joined by tools/kernel_hbm.py into gpurun_out/hbm_<name>_<TAG>.{txt,json}.
 # (C2's k_link: bench.py's own FETCH_SIZE / WRITE_SIZE passes, roofline.traffic.)
-#   tools/gpu_pmc_all.sh TAG
+#   tools/gpu_pmc_all.sh TAG [c3 c5 json proto3]   (default: all four)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 TAG=${1:-r03}
@@ -19,8 +19,14 @@ run() {  # name timeout command...
     $O/hf_${n}_$TAG $O/hw_${n}_$TAG --json $O/hbm_${n}_$TAG.json --label "$n" > $O/hbm_${n}_$TAG.txt
 }
 B="bench.py --steps 3 --warmup 1 --inflight 1 --no-parity --no-cpu-baseline --no-traffic --no-c5"
-run c3 300 python3 $B --config c3 || exit $?
-run c5 400 python3 tools/c5_run.py --no-parity --steps 2 --host-threads 1 || exit $?
-run json 240 python3 tools/json_decode_run.py --reps 2 || exit $?
-run proto3 240 python3 tools/json_decode_run.py --reps 2 --format proto3 || exit $?
+shift
+WHICH=${*:-c3 c5 json proto3}
+for n in $WHICH; do
+  case $n in
+    c3) run c3 300 python3 $B --config c3 || exit $? ;;
+    c5) run c5 400 python3 tools/c5_run.py --no-parity --steps 2 --host-threads 1 || exit $? ;;
+    json) run json 240 python3 tools/json_decode_run.py --reps 2 || exit $? ;;
+    proto3) run proto3 240 python3 tools/json_decode_run.py --reps 2 --format proto3 || exit $? ;;
+  esac
+done
 exit 0
