@@ -43,3 +43,24 @@ def test_c4_has_messaging_and_fragments():
     kinds = (c.port_flags >> 16) & 7
     assert (kinds == 2).any() and (kinds == 3).any()
     assert (c.remote_svc >= 50).any()  # brokers
+
+
+def test_spans_of_round_trip():
+    """synth.spans_of (the facade leg's Span objects) packs back to columns that link to the same
+    links by service name - C2 and C4 (messaging, fragments, errors) - as the original columns."""
+    from oracle import ref
+    from zipkin_amd.columnar import Dictionary, pack_traces
+    for w in (synth.C2.scaled(2000), synth.C4.scaled(2000)):
+        cols = synth.generate(w)
+        traces = synth.spans_of(cols, w, cols.n_traces)
+        svc, ip4, ip6 = Dictionary(), Dictionary(), Dictionary()
+        back = pack_traces(traces, svc, ip4, ip6)
+        assert back.n_spans == cols.n_spans
+        names = synth.service_names(w)
+        st, p, c, n, e = ref.link(cols, threads=2)
+        assert st == 0
+        exp = sorted(zip([names[i] for i in p], [names[i] for i in c], n.tolist(), e.tolist()))
+        st, p, c, n, e = ref.link(back, threads=2)
+        assert st == 0
+        got = sorted(zip([svc.strings[i] for i in p], [svc.strings[i] for i in c], n.tolist(), e.tolist()))
+        assert got == exp and len(exp) > 10
