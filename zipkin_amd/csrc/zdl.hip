@@ -1717,6 +1717,7 @@ struct zdl_ctx {
   hipStream_t side = nullptr;
   hipEvent_t side_ev = nullptr;
   bool big_side = false;
+  bool giant_fused = true;  // ZDL_GIANT_FUSED=0: k_g_join's answers through b_id to k_g_par (A/B)
   uint64_t gg_ntmax = 0;
   uint32_t* h_gmeta = nullptr;  // pinned: the tier's GM_* words
   int big_exact = 0;
@@ -2004,7 +2005,9 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
                                 (int)link_block_bytes(m == 3 ? 0 : w, tm, m));
   }
   if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)k_g_join, hipFuncAttributeMaxDynamicSharedMemorySize, GHCAP * 16);
+    e = hipFuncSetAttribute((const void*)k_g_join<true>, hipFuncAttributeMaxDynamicSharedMemorySize, GHCAP * 16);
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)k_g_join<false>, hipFuncAttributeMaxDynamicSharedMemorySize, GHCAP * 16);
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)k_big<TAIL_WG>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)std::max(tail_block_bytes(0), std::max(tail_block_bytes(1), tail_block_bytes(2))));
@@ -2035,6 +2038,8 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
     c->big_exact = be && be[0] == '1';
     const char* bs = getenv("ZDL_BIG_SIDE");
     c->big_side = bs && bs[0] == '1';
+    const char* gf = getenv("ZDL_GIANT_FUSED");
+    c->giant_fused = !(gf && gf[0] == '0');
     const char* wb = getenv("ZDL_WAVE_BIG");
     c->wave_big = !(wb && wb[0] == '0');
     const char* gm = getenv("ZDL_GIANT_MIN");
@@ -2515,14 +2520,23 @@ static int giant_run(zdl_ctx* c, Args& A) {
   hipLaunchKernelGGL(k_g_hist, tg, tb, 0, s, A, G);
   hipLaunchKernelGGL(k_g_scan, dim3(std::min<uint32_t>(ng, (uint32_t)c->cus * 4)), dim3(BIG_WG), 0, s, A, G);
   hipLaunchKernelGGL(k_g_scatter, tg, tb, 0, s, A, G);
-  hipLaunchKernelGGL(k_g_join, tg, tb, GHCAP * 16, s, A, G);
-  hipLaunchKernelGGL(k_g_par, tg, tb, 0, s, A, G);
+  if (c->giant_fused) {
+    hipLaunchKernelGGL(k_g_join<true>, tg, tb, GHCAP * 16, s, A, G);
+  } else {
+    hipLaunchKernelGGL(k_g_join<false>, tg, tb, GHCAP * 16, s, A, G);
+    hipLaunchKernelGGL(k_g_par, tg, tb, 0, s, A, G);
+  }
   // after r rounds of two hops a points at least 3^r generations up: enough once 3^r >= the
-  // depth (<= n); rounds after convergence return at once (the flag)
+  // depth (<= n); rounds after convergence return at once (the flag). (After the fused join,
+  // round 0 reads every pending word as the root index k_g_par would have written: the same
+  // values, the same count.)
   int rounds = 1;
   for (uint64_t reach = 3; reach < (uint64_t)maxn && rounds < GROUNDS_MAX; reach *= 3) ++rounds;
   const dim3 jg(jgrid);  // persistent; a multiple of 8 (8 * G.per = 8 * ceil(nt / 8))
-  for (int r = 0; r < rounds; ++r) hipLaunchKernelGGL(k_g_jump, jg, tb, 0, s, A, G, r);
+  for (int r = 0; r < rounds; ++r) {
+    if (r == 0 && c->giant_fused) hipLaunchKernelGGL(k_g_jump<true>, jg, tb, 0, s, A, G, r);
+    else hipLaunchKernelGGL(k_g_jump<false>, jg, tb, 0, s, A, G, r);
+  }
   hipLaunchKernelGGL(k_g_rules, tg, tb, 0, s, A, G);
   HIP_TRY(c, hipGetLastError());
   return ZDL_OK;
