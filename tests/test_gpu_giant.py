@@ -146,6 +146,36 @@ def test_not_simple_and_cycles(monkeypatch):
     assert _link(cols, 10_000) == exp
 
 
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_root_attachment(fused, monkeypatch):
+    """Spans that attach to the root (shared spans without a client, non-shared ones whose parent
+    is missing, extra parentless spans): the fused join leaves them pending for k_g_jump's round
+    0, which must read the root's index and kind as k_g_par wrote them (ZDL_GIANT_FUSED=0).
+    Cases: a root with no kind (its nearest-kinded-ancestor pointer passes through it), a
+    trace with no parentless span at all (a cycle through the root), many parentless spans and
+    orphaned subtrees in one trace."""
+    monkeypatch.setenv("ZDL_GIANT_FUSED", fused)
+    monkeypatch.setenv("ZDL_GIANT_MIN", "192")
+    kind_mask = np.uint32(7 << N.PF_KIND_SHIFT)
+    a = _copy(_giant(40, 5000))  # the root loses its kind
+    r = np.nonzero(a.parent_id == 0)[0]
+    a.port_flags[r] |= kind_mask  # (ZDL_KIND_NULL = 7)
+    b = _copy(_giant(41, 6000))  # the root gets a parent inside its own tree: no root
+    r = np.nonzero(b.parent_id == 0)[0][0]
+    b.parent_id[r] = b.id[len(b.id) - 1]
+    c = _copy(_giant(42, 7000))  # every 50th parented span loses its parent (missing-id attach)
+    nsp = np.nonzero(c.parent_id != 0)[0][::50]
+    c.parent_id[nsp] = np.uint64(0xABCDEF0000000000) + np.arange(len(nsp), dtype=np.uint64)
+    d = _copy(_giant(43, 4000))  # extra parentless spans, and parentless spans with no kind
+    nsp = np.nonzero(d.parent_id != 0)[0]
+    d.parent_id[nsp[::40]] = 0
+    d.port_flags[nsp[::80]] |= kind_mask
+    cols = concat_columns([a, b, c, d, _giant(44, 3000)])
+    assert _link(cols, 10_000) == _oracle(cols)
+    win = (int(cols.timestamp.max()) // 1000 + 1, 10**9)  # every trace in: the window's code path
+    assert _link(cols, 10_000, window=win) == _oracle(cols, window=win)
+
+
 @pytest.mark.parametrize("gmin", ["192", "1024"])
 def test_messy_big_traces_vs_cpp(gmin, monkeypatch):
     """C4's faults in traces of 200-3000 spans on a sparse context (ZDL_SPARSE=1 at 54
