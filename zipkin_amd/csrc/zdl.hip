@@ -1717,7 +1717,10 @@ struct zdl_ctx {
   hipStream_t side = nullptr;
   hipEvent_t side_ev = nullptr;
   bool big_side = false;
-  bool giant_fused = true;  // ZDL_GIANT_FUSED=0: k_g_join's answers through b_id to k_g_par (A/B)
+  // ZDL_GIANT_FUSED=1: k_g_par fused into k_g_join (zdl_giant.inc; 1.44 -> 1.40 ms of tier
+  // kernels at C5). Off: one run of the tree-stream giant test faulted the GPU with it (two
+  // passed, cause not found), and the two-kernel path is the one validated over rounds 3-5.
+  bool giant_fused = false;
   uint64_t gg_ntmax = 0;
   uint32_t* h_gmeta = nullptr;  // pinned: the tier's GM_* words
   int big_exact = 0;
@@ -2039,7 +2042,7 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
     const char* bs = getenv("ZDL_BIG_SIDE");
     c->big_side = bs && bs[0] == '1';
     const char* gf = getenv("ZDL_GIANT_FUSED");
-    c->giant_fused = !(gf && gf[0] == '0');
+    c->giant_fused = gf && gf[0] == '1';
     const char* wb = getenv("ZDL_WAVE_BIG");
     c->wave_big = !(wb && wb[0] == '0');
     const char* gm = getenv("ZDL_GIANT_MIN");
