@@ -602,6 +602,156 @@ def cpu_info():
     return {"nproc": nproc, "affinity": aff, "quota": quota, "usable": usable, "model": model, "why": why}
 
 
+def c3_job_leg(device, ranks=8, traces_per_rank=C3_TRACES_PER_GPU, steps=5, parity=True, threads=16):
+    """BASELINE.json configs[2] as stated - 1B synthetic spans / 100M traces / 500 services sharded
+    by splitmix64(trace_lo) over 8 ranks, the ranks' counts combined (DependencyLinker.merge's sum,
+    DependencyLinker.java:189-204) - on ONE MI355X: the 8 ranks are contexts of this process joined
+    by zdl_comm_init_local (zipkin_amd/csrc/zdl_xport.inc), so every rank's put, its LOG reduce and
+    the job's sum all-reduce run the code of an 8-GPU job; only the combine's bytes move by device
+    copies instead of xGMI.
+
+    1. the whole batch is generated in host memory, and split into the 8 shards by the device
+       group's host split (zdl_shard.h, timed: `host_split`, SURVEY §8(e)'s named scaling risk);
+    2. each shard goes to HBM, and the C++ restatement links it on the host (parity, summed);
+    3. `ms_per_job_step`: the 8 ranks' reset + put + link on 8 host threads, median of `steps`;
+    4. `phased`: the same with a barrier between the puts and the links, so the link phase
+       (the local sum all-reduce + compaction + read-back) is timed apart from the puts; and one
+       rank's shard linked on a context outside the world, for the link without a combine."""
+    import threading
+
+    import torch
+    from zipkin_amd import _native as N
+    from zipkin_amd import synth
+    w = synth.C3.scaled(ranks * traces_per_rank)
+    S = w.total_services
+    t0 = time.perf_counter()
+    full = synth.generate(w, threads=threads)
+    gen_s = time.perf_counter() - t0
+    n_spans, n_traces = full.n_spans, full.n_traces
+    shards, split_s = synth.shard_host(full, ranks, threads=threads, timestamps=False)
+    split_bytes = 2 * (BYTES_PER_SPAN * n_spans + BYTES_PER_TRACE * (n_traces + 1))
+    host_split = {"seconds": split_s, "spans": n_spans, "shards": ranks, "threads": threads,
+                  "spans_per_s": n_spans / split_s, "host_gbs": split_bytes / split_s / 1e9,
+                  "note": "zdl_shard.h plan + scatter (what zdl_put_spans on a device group runs on the host before "
+                          "its uploads): 44 B/span + 8 B/trace read and written; host memory bandwidth bound"}
+    del full
+    log(f"c3 job: generated {n_spans} spans in {gen_s:.1f}s; host split into {ranks} shards {split_s:.2f}s "
+        f"({n_spans / split_s:.3e} spans/s on {threads} threads)")
+    dev = torch.device("cuda", device)
+    names = ("id", "parent_id", "local_svc", "remote_svc", "local_ip4", "local_ip6", "port_flags")
+    dcols, doffs, meta = [], [], []
+    call = np.zeros(S * S, np.int64)
+    err = np.zeros(S * S, np.int64)
+    oracle_s = 0.0
+    for r in range(ranks):
+        cols = shards[r]
+        dcols.append({k: torch.from_numpy(np.ascontiguousarray(getattr(cols, k)).view(
+            np.int64 if getattr(cols, k).dtype.itemsize == 8 else np.int32)).to(dev) for k in names})
+        doffs.append(torch.from_numpy(cols.offsets.view(np.int64)).to(dev))
+        meta.append((cols.n_spans, cols.n_traces))
+        if parity:
+            from oracle import ref
+            t1 = time.perf_counter()
+            st, op, oc, on, oe = ref.link(cols, threads=threads)
+            oracle_s += time.perf_counter() - t1
+            assert st == 0, st
+            np.add.at(call, op.astype(np.int64) * S + oc, on)
+            np.add.at(err, op.astype(np.int64) * S + oc, oe)
+        shards[r] = None
+    torch.cuda.synchronize(dev)
+    ctxs = [N.Context(S, device=device) for _ in range(ranks)]
+    N.Context.comm_init_local(ctxs)
+
+    def put(r):
+        p = {k: v.data_ptr() for k, v in dcols[r].items()}
+        ctxs[r].reset()
+        ctxs[r].put_spans_device(p, meta[r][0], doffs[r].data_ptr(), meta[r][1])
+
+    out = [None] * ranks
+    bar = threading.Barrier(ranks)
+    marks = [[0.0, 0.0, 0.0] for _ in range(ranks)]
+
+    def step(phased):
+        errs = []
+
+        def run(r):
+            try:
+                put(r)
+                if phased:
+                    ctxs[r].sync()
+                    marks[r][0] = time.perf_counter()
+                    bar.wait()
+                    marks[r][1] = time.perf_counter()
+                out[r] = ctxs[r].link()
+                marks[r][2] = time.perf_counter()
+            except Exception as ex:  # noqa: BLE001
+                errs.append((r, repr(ex)))
+                bar.abort()
+
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        th = [threading.Thread(target=run, args=(r,)) for r in range(ranks)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        if errs:
+            raise RuntimeError(f"c3 job: rank failure {errs}")
+        t2 = time.perf_counter()
+        if not phased:
+            return (t2 - t1) * 1e3, None, None
+        puts = max(m[0] for m in marks) - t1
+        links = max(m[2] for m in marks) - max(m[1] for m in marks)
+        return (t2 - t1) * 1e3, puts * 1e3, links * 1e3
+
+    step(False)  # warmup
+    job = [step(False)[0] for _ in range(steps)]
+    ph = [step(True) for _ in range(steps)]
+    ranks_agree = all(all(np.array_equal(a, b) for a, b in zip(out[0], out[r])) for r in range(ranks))
+    for c in ctxs:
+        c.close()
+    # the link of one rank's shard without a combine: a context outside the world
+    solo = N.Context(S, device=device)
+    sl = []
+    for _ in range(steps + 1):
+        p = {k: v.data_ptr() for k, v in dcols[0].items()}
+        solo.reset()
+        solo.put_spans_device(p, meta[0][0], doffs[0].data_ptr(), meta[0][1])
+        solo.sync()
+        t1 = time.perf_counter()
+        solo.link()
+        sl.append((time.perf_counter() - t1) * 1e3)
+    solo.close()
+    del dcols, doffs
+    torch.cuda.empty_cache()
+    ms = float(np.median(job))
+    link_phase = float(np.median([x[2] for x in ph]))
+    solo_link = float(np.median(sl[1:]))
+    res = {"workload": "c3_1B_spans_100M_traces_500_services as BASELINE.json states it: an 8-rank job on one "
+                       "MI355X (zdl_comm_init_local; the ranks' bytes move by device copies, not xGMI)",
+           "ranks": ranks, "spans": n_spans, "traces": n_traces, "services": S, "steps": steps,
+           "ms_per_job_step": ms, "spans_per_s": n_spans / (ms * 1e-3),
+           "step_roofline_frac": (BYTES_PER_SPAN * n_spans + BYTES_PER_TRACE * (n_traces + ranks)) / (ms * 1e-3) / 1e9
+           / HBM_PEAK_GBS,
+           "phased": {"ms_per_job_step": float(np.median([x[0] for x in ph])),
+                      "puts_ms": float(np.median([x[1] for x in ph])),
+                      "link_phase_ms": link_phase, "solo_link_ms": solo_link,
+                      "combine_ms": max(link_phase - solo_link, 0.0),
+                      "note": "puts: step start to the last rank's put done (8 ranks' k_link + LOG reduce on one GPU); "
+                              "link phase: every rank's zdl_link after a barrier (the local sum all-reduce of the "
+                              "500 x 500 tables + compaction + read-back), max over ranks; combine = link phase - "
+                              "the same link on a context outside the world"},
+           "host_split": host_split, "generate_s": gen_s, "links": int(len(out[0][0])), "ranks_agree": ranks_agree}
+    if parity:
+        nz = np.nonzero(call)[0]
+        exp = sorted(zip((nz // S).tolist(), (nz % S).tolist(), call[nz].tolist(), err[nz].tolist()))
+        got = sorted(zip(*(a.tolist() for a in out[0])))
+        res["parity"] = "bit-exact vs the C++ restatement over every span" if got == exp and ranks_agree else "MISMATCH"
+        res["oracle_s"] = oracle_s
+        res["calls"] = int(call.sum())
+    return res
+
+
 def h2d_leg(cols, S, device, reps=3):
     """Host-buffer side of the path (not `value`): the batch's 44 B/span columns + offsets
     copied from pinned host memory (the PCIe rate a JNI caller with pinned buffers gets), and
@@ -657,6 +807,9 @@ def main():
     ap.add_argument("--no-store", action="store_true", help="skip the resident-store getDependencies side leg")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 (high-cardinality) side leg")
     ap.add_argument("--no-put-trace", action="store_true", help="skip the per-trace putTrace loop side leg")
+    ap.add_argument("--no-c3-job", action="store_true",
+                    help="skip the 1B-span C3 job side leg (8 ranks as a local world on this GPU)")
+    ap.add_argument("--c3-job-traces", type=int, default=C3_TRACES_PER_GPU, help=argparse.SUPPRESS)
     ap.add_argument("--c5-host-threads", type=int, default=2, choices=(1, 2),
                     help="C5 leg: one host thread per context (2) or one alternating both (1)")
     ap.add_argument("--no-traffic", action="store_true",
@@ -947,6 +1100,14 @@ def main():
         c5 = c5_leg(local, parity=not args.no_parity, threads=cpu_info()["usable"], host_threads=args.c5_host_threads)
         log(f"c5: {c5['ms_per_step']:.2f} ms/step ({c5['spans_per_s']:.3e} spans/s), links {c5['parity']}, "
             + ", ".join(f"{k} {v['ms']:.3f} ms" for k, v in c5["phases"].items() if v["ms"] is not None))
+    c3job = None
+    if side and not args.no_c3_job:
+        c3job = c3_job_leg(local, traces_per_rank=args.c3_job_traces, parity=not args.no_parity,
+                           threads=cpu_info()["usable"])
+        log(f"c3 job (1B spans, 8 ranks on one GPU): {c3job['ms_per_job_step']:.2f} ms/job step "
+            f"({c3job['spans_per_s']:.3e} spans/s), puts {c3job['phased']['puts_ms']:.2f} ms, link phase "
+            f"{c3job['phased']['link_phase_ms']:.2f} ms (combine {c3job['phased']['combine_ms']:.2f} ms), "
+            f"links {c3job.get('parity')}")
     parity = None
     cpu = None
     if rank == 0 and world == 1 and not args.no_parity:
@@ -1026,7 +1187,7 @@ def main():
                        "parity": parity, "links": int(len(p)), "insertion_order": ins, "host_buffers": h2d,
                        "proto3_ingest": p3, "json_v2_ingest": jleg, "store_get_dependencies": sleg,
                        "mysql_rows": rows_leg, "put_trace_loop": ptl, "put_trace_loop_c4": ptc4, "facade_put_trace_python": fpt,
-                       "c5": c5},
+                       "c5": c5, "c3_job": c3job},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "k_link", "algorithmic_bytes_per_launch": klink_bytes,

@@ -381,7 +381,7 @@ class DependencyLinker:
             if cs is None:
                 self._fine("skipping fake root node for broken span tree")
                 continue
-            self._fine(f"processing {cs}")
+            self._fine(f"processing {cs.to_json_v2()}")  # Span.toString(): JSON_V2 (Span.java:622-624)
             kind = cs.kind
             if kind == Kind.CLIENT and current.children:
                 continue
@@ -430,7 +430,7 @@ class DependencyLinker:
         while a is not None:
             s = a.span
             if s is not None and s.kind is not None:
-                self._fine(f"found remote ancestor {s}")
+                self._fine(f"found remote ancestor {s.to_json_v2()}")
                 return s
             a = a.parent
         return None

@@ -262,3 +262,16 @@ def test_gpu_daily_sorted_skips_other_ranges(sparse, monkeypatch):
     got = daily.aggregate_links(out, insertion_order=False)
     assert 0 in got and len(got) >= 8
     assert _as_sorted_sets(got) == _as_sorted_sets(O.aggregate_links(out))
+
+
+@pytest.mark.gpu
+def test_gpu_daily_sparse_10k_services_40_days():
+    """10 000 services over 40 days: more days than one sparse context's cells hold (2^31 /
+    10^8 = 21), so two ranges link the same store-resident batch (zdl_put_stored through a
+    host grouping permutation); every day against the oracle."""
+    from zipkin_amd import daily
+    sp = _high_cardinality_spans(977, 4000, 10_000, 40)
+    got = daily.aggregate_links(sp, insertion_order=False)
+    want = O.aggregate_links(sp)
+    assert len(got) == 40
+    _assert_same_days(got, want)

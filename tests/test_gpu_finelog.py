@@ -2,8 +2,8 @@
 145-147, 227-231) rendered from the device's reason codes (zdl_tree_reasons): the messages the
 reference's tests assert (DependencyLinkerTest.java:90, 394, and the fake-root / missing-link
 cases; SpanNodeTest's exact builder logs), and the whole message sequence against the oracle's
-restatement on random traces. "processing <span>" / "found remote ancestor <span>" are compared
-by position only: the oracle quotes its own span repr, the facade the first fragment's JSON."""
+restatement on random traces, text included: "processing <span>" / "found remote ancestor <span>"
+quote Span.toString() (JSON v2) of the span Trace.merge left, fragments merged."""
 import logging
 import random
 
@@ -98,5 +98,31 @@ def test_random_traces_log_sequence_matches_oracle(seed):
         ref.put_trace(t)
     msgs, links = _device_log(traces, batch=bool(seed % 2), name=f"r{seed}")
     assert _shape(msgs) == _shape(ref_log)
+    assert msgs == ref_log
     assert [(l.parent, l.child, l.call_count, l.error_count) for l in links] == \
         [(l.parent, l.child, l.call_count, l.error_count) for l in ref.link()]
+
+
+def test_processing_quotes_the_merged_span():
+    """A server span sent in two fragments (name and timestamp in one, endpoint and tags in the
+    other) and a shared span without a parent id behind its client: "processing" quotes the
+    span Trace.merge made (Trace.java:42-84), the ancestor line the client after the merge."""
+    from zipkin_amd.model import Endpoint, Kind, Span
+    fe, be = Endpoint.create("frontend"), Endpoint.create("backend")
+    t = [Span.create("000000000000000a", "1", None, Kind.SERVER, name="get", timestamp=1_000_000,
+                     local_endpoint=fe),
+         Span.create("a", "1", None, None, duration=50, tags={"http.path": "/"}),
+         Span.create("a", "2", "1", Kind.CLIENT, name="call", local_endpoint=fe, remote_endpoint=be),
+         Span.create("a", "2", None, Kind.SERVER, shared=True, local_endpoint=be)]
+    msgs, links = _device_log([t], name="merged")
+    root = ('{"traceId":"000000000000000a","id":"0000000000000001","kind":"SERVER","name":"get",'
+            '"timestamp":1000000,"duration":50,"localEndpoint":{"serviceName":"frontend"},'
+            '"tags":{"http.path":"/"}}')
+    server = ('{"traceId":"000000000000000a","parentId":"0000000000000001","id":"0000000000000002",'
+              '"kind":"SERVER","localEndpoint":{"serviceName":"backend"},"shared":true}')
+    assert f"processing {root}" in msgs
+    assert f"processing {server}" in msgs
+    ref_log = []
+    O.DependencyLinker(ref_log).put_trace(t)
+    assert msgs == ref_log
+    assert [(l.parent, l.child, l.call_count) for l in links] == [("frontend", "backend", 1)]

@@ -14,7 +14,6 @@ cannot link exactly to k_tail's exact path:
 * ids crafted so that one join bucket overflows its LDS hash (exact path);
 * C4's faults (split spans, missing brokers, extra roots) in traces of 200-3000 spans.
 """
-import os
 
 import numpy as np
 import pytest
@@ -148,19 +147,12 @@ def test_not_simple_and_cycles(monkeypatch):
     assert _link(cols, 10_000) == exp
 
 
-_FUSED_OPT_IN = pytest.mark.skipif(os.environ.get("ZDL_TEST_GIANT_FUSED") != "1",
-                                   reason="the fused join is opt-in (DESIGN.md §2.9): ZDL_TEST_GIANT_FUSED=1")
-
-
-@pytest.mark.parametrize("fused", [pytest.param("1", marks=_FUSED_OPT_IN), "0"])
-def test_root_attachment(fused, monkeypatch):
+def test_root_attachment(monkeypatch):
     """Spans that attach to the root (shared spans without a client, non-shared ones whose parent
-    is missing, extra parentless spans): the fused join leaves them pending for k_g_jump's round
-    0, which must read the root's index and kind as k_g_par wrote them (ZDL_GIANT_FUSED=0).
+    is missing, extra parentless spans), which k_g_par resolves from the join's root index.
     Cases: a root with no kind (its nearest-kinded-ancestor pointer passes through it), a
     trace with no parentless span at all (a cycle through the root), many parentless spans and
     orphaned subtrees in one trace."""
-    monkeypatch.setenv("ZDL_GIANT_FUSED", fused)
     monkeypatch.setenv("ZDL_GIANT_MIN", "192")
     kind_mask = np.uint32(7 << N.PF_KIND_SHIFT)
     a = _copy(_giant(40, 5000))  # the root loses its kind

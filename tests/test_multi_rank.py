@@ -88,3 +88,51 @@ def test_partition_keeps_mixed_width_trace_ids_together():
     cols = pack_traces([t], Dictionary(), Dictionary(), Dictionary())
     parts = shard.partition_columns(cols, 4)
     assert sorted(p.n_spans for p in parts) == [0, 0, 0, 3]
+
+
+def _same_columns(a, b):
+    for k in ("trace_lo", "id", "parent_id", "local_svc", "remote_svc", "local_ip4", "local_ip6", "port_flags",
+              "timestamp"):
+        assert np.array_equal(getattr(a, k), getattr(b, k)), k
+    # partition_columns keeps empty traces (the host split drops them: they link nothing)
+    assert np.array_equal(a.offsets, np.unique(b.offsets))
+
+
+def test_host_split_equals_partition_columns():
+    """A device group's host split (zdl_shard.h, run by libzdl's group_put; here through
+    libzdl_synth) gives every shard exactly shard.partition_columns' traces, in storage order,
+    with the same CSR offsets - at 1, 2, 3, 8 and 64 shards, on 1 and 4 threads, with empty
+    traces (which go nowhere) mixed in."""
+    from zipkin_amd.columnar import Columns
+    cols = synth.generate(synth.C4.scaled(6000), threads=2)
+    sizes = np.diff(cols.offsets.astype(np.int64))
+    # empty traces inserted every 97th trace
+    new_sizes = np.insert(sizes, np.arange(0, len(sizes), 97), 0)
+    off = np.zeros(len(new_sizes) + 1, np.uint64)
+    off[1:] = np.cumsum(new_sizes)
+    holey = Columns(cols.trace_lo, cols.id, cols.parent_id, cols.local_svc, cols.remote_svc, cols.local_ip4,
+                    cols.local_ip6, cols.port_flags, cols.timestamp, off)
+    for c in (cols, holey):
+        for n in (1, 2, 3, 8, 64):
+            want = shard.partition_columns(c, n)
+            for th in (1, 4):
+                got, sec = synth.shard_host(c, n, threads=th)
+                assert sec >= 0 and len(got) == n
+                for g, w in zip(got, want):
+                    _same_columns(g, w)
+
+
+def test_host_split_ungrouped_keeps_input_order():
+    """Ungrouped input (no offsets): every span by its own trace_lo, input order kept."""
+    cols = synth.generate(synth.C2.scaled(3000), threads=2)
+    perm = np.random.default_rng(5).permutation(cols.n_spans)
+    from zipkin_amd.columnar import Columns
+    sh = Columns(*(getattr(cols, k)[perm] for k in ("trace_lo", "id", "parent_id", "local_svc", "remote_svc",
+                                                    "local_ip4", "local_ip6", "port_flags", "timestamp")),
+                 np.zeros(1, np.uint64))
+    got, _ = synth.shard_host(sh, 5, threads=3, grouped=False)
+    d = shard.shard_of(sh.trace_lo, 5)
+    for r in range(5):
+        assert np.array_equal(got[r].id, sh.id[d == r])
+        assert np.array_equal(got[r].trace_lo, sh.trace_lo[d == r])
+        assert np.array_equal(got[r].port_flags, sh.port_flags[d == r])

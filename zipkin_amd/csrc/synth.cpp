@@ -573,3 +573,45 @@ int zdl_synth_put_trace_loop(int (*put)(zdl_ctx*, const zdl_span_cols*, uint64_t
 }
 
 }  // extern "C"
+
+#include <chrono>
+
+#include "zdl_shard.h"
+
+extern "C" {
+
+// A device group's host split (zdl_shard.h, the code libzdl's group_put runs) on host columns:
+// zdl_synth_shard_plan sizes the shards (spans, traces per shard), zdl_synth_shard plans and
+// scatters into the caller's columns - out[d] (columns of spans[d] entries; off: traces[d] + 1
+// entries, or NULL for ungrouped input) - and returns its wall-clock seconds (plan + scatter).
+void zdl_synth_shard_plan(const zdl_span_cols* in, uint64_t n_spans, const uint64_t* off, uint64_t n_traces,
+                          uint32_t n_shards, int threads, uint64_t* spans, uint64_t* traces) {
+  const zdl_shard::In x{in->trace_lo,  in->id,        in->parent_id,  in->local_svc, in->remote_svc,
+                        in->local_ip4, in->local_ip6, in->port_flags, in->timestamp, in->ord};
+  const zdl_shard::Plan p = zdl_shard::plan(x, n_spans, off, n_traces, n_shards, threads);
+  for (uint32_t d = 0; d < n_shards; ++d) {
+    spans[d] = p.spans[d];
+    traces[d] = p.traces[d];
+  }
+}
+
+double zdl_synth_shard(const zdl_span_cols* in, uint64_t n_spans, const uint64_t* off, uint64_t n_traces,
+                       uint32_t n_shards, int threads, const zdl_span_cols* out, uint64_t* const* out_off) {
+  const auto t0 = std::chrono::steady_clock::now();
+  const zdl_shard::In x{in->trace_lo,  in->id,        in->parent_id,  in->local_svc, in->remote_svc,
+                        in->local_ip4, in->local_ip6, in->port_flags, in->timestamp, in->ord};
+  const zdl_shard::Plan p = zdl_shard::plan(x, n_spans, off, n_traces, n_shards, threads);
+  std::vector<zdl_shard::Out> o(n_shards);
+  for (uint32_t d = 0; d < n_shards; ++d)
+    o[d] = zdl_shard::Out{const_cast<uint64_t*>(out[d].trace_lo), const_cast<uint64_t*>(out[d].id),
+                          const_cast<uint64_t*>(out[d].parent_id), const_cast<int32_t*>(out[d].local_svc),
+                          const_cast<int32_t*>(out[d].remote_svc), const_cast<int32_t*>(out[d].local_ip4),
+                          const_cast<int32_t*>(out[d].local_ip6), const_cast<uint32_t*>(out[d].port_flags),
+                          const_cast<int64_t*>(out[d].timestamp), const_cast<uint32_t*>(out[d].ord),
+                          off ? out_off[d] : nullptr};
+  zdl_shard::scatter(x, off, p, o.data(), threads);
+  return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
+}  // extern "C"
+

@@ -27,6 +27,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <thread>
 #include <vector>
@@ -35,6 +36,7 @@
 #include "zdl_algo.h"
 #include "zdl_sparse.h"
 #include "zdl_xplan.h"
+#include "zdl_shard.h"
 
 namespace zdl {
 
@@ -1710,17 +1712,6 @@ struct zdl_ctx {
   DevBuf<uint8_t> gg_stat;
   GArgs gg_args{};            // the tier's arguments, from giant_prep to giant_run
   hipEvent_t gg_ev = nullptr;  // k_g_prep's totals copied to h_gmeta
-  // ZDL_BIG_SIDE=1: k_big beside k_mid and the giant tier on a stream of its own, joined before
-  // k_tail. Measured at C5 (8 HW queues, bit-exact): one put alone 6.68 -> 6.49 ms, two contexts
-  // in flight 4.74 -> 4.97 ms (the kernels share the CUs, k_big<1024>'s 150 KB of LDS keeps the
-  // tier's workgroups off its CU, and a third and fourth stream share the hardware queues). Off.
-  hipStream_t side = nullptr;
-  hipEvent_t side_ev = nullptr;
-  bool big_side = false;
-  // ZDL_GIANT_FUSED=1: k_g_par fused into k_g_join (zdl_giant.inc; 1.44 -> 1.40 ms of tier
-  // kernels at C5). Off: one run of the tree-stream giant test faulted the GPU with it (two
-  // passed, cause not found), and the two-kernel path is the one validated over rounds 3-5.
-  bool giant_fused = false;
   uint64_t gg_ntmax = 0;
   uint32_t* h_gmeta = nullptr;  // pinned: the tier's GM_* words
   int big_exact = 0;
@@ -1910,6 +1901,7 @@ static int stage_flush(zdl_ctx* c);                // zdl_put_trace's staged tra
 static void stage_drop(zdl_ctx* c);                // ... discarded (zdl_reset)
 static void stage_free(zdl_ctx* c);
 static int rec_wait(zdl_ctx* c);  // the SDMA record copy of the last link (ZDL_REC_SDMA)
+static int x_failed(zdl_ctx* c, int rc);  // a failed combine breaks a local world (zdl_xport.inc)
 
 // splitmix64 finaliser (shard.py's): trace t goes to device splitmix64(trace_lo) % n
 inline uint64_t splitmix64(uint64_t x) {
@@ -2008,9 +2000,7 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
                                 (int)link_block_bytes(m == 3 ? 0 : w, tm, m));
   }
   if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)k_g_join<true>, hipFuncAttributeMaxDynamicSharedMemorySize, GHCAP * 16);
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)k_g_join<false>, hipFuncAttributeMaxDynamicSharedMemorySize, GHCAP * 16);
+    e = hipFuncSetAttribute((const void*)k_g_join, hipFuncAttributeMaxDynamicSharedMemorySize, GHCAP * 16);
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)k_big<TAIL_WG>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)std::max(tail_block_bytes(0), std::max(tail_block_bytes(1), tail_block_bytes(2))));
@@ -2039,10 +2029,6 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
     c->skip = sk ? (uint32_t)strtoul(sk, nullptr, 0) : 0u;
     const char* be = getenv("ZDL_BIG_EXACT");
     c->big_exact = be && be[0] == '1';
-    const char* bs = getenv("ZDL_BIG_SIDE");
-    c->big_side = bs && bs[0] == '1';
-    const char* gf = getenv("ZDL_GIANT_FUSED");
-    c->giant_fused = gf && gf[0] == '1';
     const char* wb = getenv("ZDL_WAVE_BIG");
     c->wave_big = !(wb && wb[0] == '0');
     const char* gm = getenv("ZDL_GIANT_MIN");
@@ -2155,8 +2141,6 @@ void zdl_destroy(zdl_ctx* c) {
   c->gg_part32.release();
   c->gg_part64.release();
   if (c->gg_ev) (void)hipEventDestroy(c->gg_ev);
-  if (c->side_ev) (void)hipEventDestroy(c->side_ev);
-  if (c->side) (void)hipStreamDestroy(c->side);
   c->gg_base.release(); c->gg_h0.release(); c->gg_root.release(); c->gg_tsroot.release(); c->gg_tsmin.release();
   c->gg_rootidx.release(); c->gg_stat.release();
   if (c->h_gmeta) (void)hipHostFree(c->h_gmeta);
@@ -2476,28 +2460,6 @@ static int giant_prep(zdl_ctx* c, Args& A, uint64_t n_spans, uint64_t n_traces) 
   return ZDL_OK;
 }
 
-// k_big<256> and k_big<1024> on the context's side stream, behind k_g_prep (gg_ev): the back
-// list's non-giant traces, one workgroup each - latency-bound work that runs beside k_mid and the
-// giant tier instead of after them (their scratch is disjoint: every array is indexed by span
-// position at the same scale, zdl_giant.inc). side_ev joins the main stream before k_tail.
-static int launch_big_side(zdl_ctx* c, Args& A, int wmode) {
-  if (!c->side) HIP_TRY(c, hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
-  if (!c->side_ev) HIP_TRY(c, hipEventCreateWithFlags(&c->side_ev, hipEventDisableTiming));
-  HIP_TRY(c, hipStreamWaitEvent(c->side, c->gg_ev, 0));
-  void* kargs[] = {&A};
-  hipError_t be = hipLaunchKernel((const void*)k_big<256>, dim3((unsigned)c->cus * 4), dim3(256), kargs,
-                                  (size_t)KB_SMALL_LDS, c->side);
-  if (be == hipSuccess)
-    be = hipLaunchKernel((const void*)k_big<TAIL_WG>, dim3(c->grid), dim3(TAIL_WG), kargs, tail_block_bytes(wmode),
-                         c->side);
-  if (be == hipSuccess) be = hipEventRecord(c->side_ev, c->side);
-  if (be != hipSuccess) {
-    c->poisoned = true;
-    return hip_fail(c, be, "k_big launch (side stream)");
-  }
-  return ZDL_OK;
-}
-
 static int giant_run(zdl_ctx* c, Args& A) {
   const hipStream_t s = c->stream;
   HIP_TRY(c, hipEventSynchronize(c->gg_ev));  // k_link and k_g_prep (k_mid may still run)
@@ -2523,23 +2485,14 @@ static int giant_run(zdl_ctx* c, Args& A) {
   hipLaunchKernelGGL(k_g_hist, tg, tb, 0, s, A, G);
   hipLaunchKernelGGL(k_g_scan, dim3(std::min<uint32_t>(ng, (uint32_t)c->cus * 4)), dim3(BIG_WG), 0, s, A, G);
   hipLaunchKernelGGL(k_g_scatter, tg, tb, 0, s, A, G);
-  if (c->giant_fused) {
-    hipLaunchKernelGGL(k_g_join<true>, tg, tb, GHCAP * 16, s, A, G);
-  } else {
-    hipLaunchKernelGGL(k_g_join<false>, tg, tb, GHCAP * 16, s, A, G);
-    hipLaunchKernelGGL(k_g_par, tg, tb, 0, s, A, G);
-  }
+  hipLaunchKernelGGL(k_g_join, tg, tb, GHCAP * 16, s, A, G);
+  hipLaunchKernelGGL(k_g_par, tg, tb, 0, s, A, G);
   // after r rounds of two hops a points at least 3^r generations up: enough once 3^r >= the
-  // depth (<= n); rounds after convergence return at once (the flag). (After the fused join,
-  // round 0 reads every pending word as the root index k_g_par would have written: the same
-  // values, the same count.)
+  // depth (<= n); rounds after convergence return at once (the flag)
   int rounds = 1;
   for (uint64_t reach = 3; reach < (uint64_t)maxn && rounds < GROUNDS_MAX; reach *= 3) ++rounds;
   const dim3 jg(jgrid);  // persistent; a multiple of 8 (8 * G.per = 8 * ceil(nt / 8))
-  for (int r = 0; r < rounds; ++r) {
-    if (r == 0 && c->giant_fused) hipLaunchKernelGGL(k_g_jump<true>, jg, tb, 0, s, A, G, r);
-    else hipLaunchKernelGGL(k_g_jump<false>, jg, tb, 0, s, A, G, r);
-  }
+  for (int r = 0; r < rounds; ++r) hipLaunchKernelGGL(k_g_jump, jg, tb, 0, s, A, G, r);
   hipLaunchKernelGGL(k_g_rules, tg, tb, 0, s, A, G);
   HIP_TRY(c, hipGetLastError());
   return ZDL_OK;
@@ -2878,17 +2831,11 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
     return ZDL_OK;
   }
   const bool giant = c->sparse && c->giant_min > 0 && !c->ord && !c->days;
-  bool big_side = false;
   if (giant) {  // the giant tier's split of the back list, before k_mid (giant_prep)
     const int grc = giant_prep(c, A, n_spans, n_traces);
     if (grc != ZDL_OK) {
       c->poisoned = true;  // k_link ran: the counter slots hold this put's counts
       return grc;
-    }
-    if (A.bstat && c->big_side) {
-      const int brc = launch_big_side(c, A, wmode);
-      if (brc != ZDL_OK) return brc;
-      big_side = true;
     }
   }
   if (A.wb_max) {  // big_list's front (WSMALL < n <= WB_MAX spans): one wave per trace
@@ -2908,13 +2855,7 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
     }
   }
   ev_record(c, 8);
-  if (big_side) {
-    const hipError_t we = hipStreamWaitEvent(c->stream, c->side_ev, 0);
-    if (we != hipSuccess) {
-      c->poisoned = true;
-      return hip_fail(c, we, "join the side stream");
-    }
-  } else if (A.bstat) {
+  if (A.bstat) {
     const int brc = launch_big(c, kargs, wmode);
     if (brc != ZDL_OK) return brc;
   }
@@ -3964,7 +3905,7 @@ int zdl_link(zdl_ctx* c, int order, zdl_links* out) {
     HIP_TRY(c, enter(c));
     if (in_job(c)) {  // a rank of a job: DependencyLinker.merge over the ranks' lists in rank order
       const int rc = comm_sum_ord(c);
-      if (rc != ZDL_OK) return rc;
+      if (rc != ZDL_OK) return x_failed(c, rc);
       return link_insertion(c, out, c->red_call.p, c->red_err.p, c->red_first.p);
     }
     return link_insertion(c, out, c->call.p, c->errc.p, c->first.p);
@@ -3973,13 +3914,13 @@ int zdl_link(zdl_ctx* c, int order, zdl_links* out) {
   HIP_TRY(c, enter(c));
   if (c->sparse && in_job(c)) {  // a rank of a job: every rank's list, summed
     const int rc = comm_sum_sparse(c);
-    if (rc != ZDL_OK) return rc;
+    if (rc != ZDL_OK) return x_failed(c, rc);
     return link_sparse(c, out, &c->gacc);
   }
   if (c->sparse) return link_sparse(c, out);
   if (in_job(c)) {  // a rank of a job: the links of every rank's tables
     const int rc = comm_sum_tables(c);
-    if (rc != ZDL_OK) return rc;
+    if (rc != ZDL_OK) return x_failed(c, rc);
     return link_sorted(c, c->red_call.p, c->red_err.p, false, out);
   }
   return link_sorted(c, c->call.p, c->errc.p, true, out);
@@ -4307,7 +4248,7 @@ int zdl_table_export(zdl_ctx* c, void* dev_call, void* dev_err) {
   }
   if (in_job(c)) {  // every rank's tables, summed
     const int rc = comm_sum_tables(c);
-    if (rc != ZDL_OK) return rc;
+    if (rc != ZDL_OK) return x_failed(c, rc);
     const size_t bytes = (size_t)c->rows * c->S * 8;
     HIP_TRY(c, hipMemcpyAsync(dev_call, c->red_call.p, bytes, hipMemcpyDeviceToDevice, c->stream));
     HIP_TRY(c, hipMemcpyAsync(dev_err, c->red_err.p, bytes, hipMemcpyDeviceToDevice, c->stream));
@@ -4428,14 +4369,8 @@ static zdl_ctx* create_group(const zdl_config* cfg) {
   return g;
 }
 
-namespace {
-template <class T>
-void gather(std::vector<T>& dst, const T* src, const std::vector<uint64_t>& idx) {
-  dst.resize(idx.size());
-  for (size_t i = 0; i < idx.size(); ++i) dst[i] = src[idx[i]];
-}
-}  // namespace
-
+// The host split (zdl_shard.h): two parallel passes over the batch (count, scatter) into one
+// column set per device, then one host thread per device uploads and launches its shard.
 int group_put(zdl_ctx* g, const zdl_span_cols* col, uint64_t n_spans, const uint64_t* off, uint64_t n_traces) {
   if (!col->trace_lo) return fail(g, ZDL_EINVAL, "device group: traces are sharded by trace_lo, which is missing");
   if (!col->id || !col->parent_id || !col->local_svc || !col->remote_svc || !col->local_ip4 || !col->local_ip6 ||
@@ -4449,42 +4384,44 @@ int group_put(zdl_ctx* g, const zdl_span_cols* col, uint64_t n_spans, const uint
   }
   if (n_spans == 0) return ZDL_OK;
   const uint32_t N = (uint32_t)g->sub.size();
-  std::vector<std::vector<uint64_t>> idx(N), toff(N);
-  for (auto& o : toff) o.push_back(0);
-  if (off) {  // whole traces, in put order: the shard of the trace's first span's trace_lo
-    for (uint64_t t = 0; t < n_traces; ++t) {
-      const uint64_t b = off[t], e = off[t + 1];
-      if (e == b) continue;
-      const uint32_t d = (uint32_t)(splitmix64(col->trace_lo[b]) % N);
-      for (uint64_t i = b; i < e; ++i) idx[d].push_back(i);
-      toff[d].push_back(idx[d].size());
-    }
-  } else {  // ungrouped: every span by its own trace_lo, input order kept
-    for (uint64_t i = 0; i < n_spans; ++i) idx[(uint32_t)(splitmix64(col->trace_lo[i]) % N)].push_back(i);
+  const int threads = zdl_shard::host_threads(getenv("ZDL_HOST_THREADS"));
+  const zdl_shard::In in{col->trace_lo, col->id,        col->parent_id,  col->local_svc, col->remote_svc,
+                         col->local_ip4, col->local_ip6, col->port_flags, col->timestamp, col->ord};
+  const zdl_shard::Plan plan = zdl_shard::plan(in, n_spans, off, n_traces, N, threads);
+  struct Shard {  // uninitialized host columns (new T[n]: the scatter writes every element)
+    std::unique_ptr<uint64_t[]> lo, id, pid, off;
+    std::unique_ptr<int32_t[]> ls, rs, i4, i6;
+    std::unique_ptr<uint32_t[]> pf, ord;
+    std::unique_ptr<int64_t[]> ts;
+  };
+  std::vector<Shard> sh(N);
+  std::vector<zdl_shard::Out> outs(N);
+  for (uint32_t d = 0; d < N; ++d) {
+    const uint64_t n = std::max<uint64_t>(plan.spans[d], 1);
+    Shard& s = sh[d];
+    s.lo.reset(new uint64_t[n]);
+    s.id.reset(new uint64_t[n]);
+    s.pid.reset(new uint64_t[n]);
+    s.ls.reset(new int32_t[n]);
+    s.rs.reset(new int32_t[n]);
+    s.i4.reset(new int32_t[n]);
+    s.i6.reset(new int32_t[n]);
+    s.pf.reset(new uint32_t[n]);
+    if (col->timestamp) s.ts.reset(new int64_t[n]);
+    if (col->ord) s.ord.reset(new uint32_t[n]);
+    if (off) s.off.reset(new uint64_t[plan.traces[d] + 1]);
+    outs[d] = zdl_shard::Out{s.lo.get(), s.id.get(), s.pid.get(), s.ls.get(), s.rs.get(), s.i4.get(),
+                             s.i6.get(), s.pf.get(), s.ts.get(), s.ord.get(), s.off.get()};
   }
+  zdl_shard::scatter(in, off, plan, outs.data(), threads);
   std::vector<int> rc(N, ZDL_OK);
   auto run = [&](uint32_t d) {
-    const std::vector<uint64_t>& ix = idx[d];
-    if (ix.empty()) return;
-    std::vector<uint64_t> lo, id, pid;
-    std::vector<int32_t> ls, rs, i4, i6;
-    std::vector<uint32_t> pf, ord;
-    std::vector<int64_t> ts;
-    gather(lo, col->trace_lo, ix);
-    gather(id, col->id, ix);
-    gather(pid, col->parent_id, ix);
-    gather(ls, col->local_svc, ix);
-    gather(rs, col->remote_svc, ix);
-    gather(i4, col->local_ip4, ix);
-    gather(i6, col->local_ip6, ix);
-    gather(pf, col->port_flags, ix);
-    if (col->timestamp) gather(ts, col->timestamp, ix);
-    if (col->ord) gather(ord, col->ord, ix);
-    zdl_span_cols sc{lo.data(), id.data(), pid.data(), ls.data(), rs.data(), i4.data(), i6.data(), pf.data(),
-                     col->timestamp ? ts.data() : nullptr, col->ord ? ord.data() : nullptr};
-    rc[d] = zdl_put_spans(g->sub[d], &sc, ix.size(), off ? toff[d].data() : nullptr, off ? toff[d].size() - 1 : 0);
+    if (plan.spans[d] == 0) return;
+    const zdl_shard::Out& o = outs[d];
+    zdl_span_cols sc{o.lo, o.id, o.pid, o.ls, o.rs, o.i4, o.i6, o.pf, o.ts, o.ord};
+    rc[d] = zdl_put_spans(g->sub[d], &sc, plan.spans[d], off ? o.off : nullptr, off ? plan.traces[d] : 0);
   };
-  std::vector<std::thread> th;  // one host thread per device: gather + upload + launch overlap
+  std::vector<std::thread> th;  // one host thread per device: upload + launch overlap
   for (uint32_t d = 0; d < N; ++d) th.emplace_back(run, d);
   for (auto& t : th) t.join();
   for (uint32_t d = 0; d < N; ++d)
@@ -4640,7 +4577,8 @@ static int comm_sum_ord(zdl_ctx* c) {
   const unsigned g = (unsigned)std::min<size_t>((SS + 255) / 256, 4096);
   // (the choice is the job's: every rank sees the same world size)
   if (world > zdl_xplan::ORD_MAX_WORLD || (lo && lo[0] == '1')) {
-    if (SS >= (1ull << 32)) return fail(c, ZDL_EINVAL, "insertion order across ranks: a table of 2^32 cells or more");
+    // (hipcub's item count is an int)
+    if (SS >= (1ull << 31)) return fail(c, ZDL_EINVAL, "insertion order across ranks: a table of 2^31 cells or more");
     HIP_TRY(c, c->ord_lk.ensure(SS));
     HIP_TRY(c, c->ord_lv.ensure(SS));
     HIP_TRY(c, c->ord_lv2.ensure(SS));

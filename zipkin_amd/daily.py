@@ -12,11 +12,14 @@ The day of a trace, the per-day (parent, child) counts and the insertion order a
 computed on the device (``zdl_set_days`` / ``zdl_link_days``); the host packs the
 columns with guessTimestamp in the timestamp column and chooses the day range.
 
-Sorted output (``insertion_order=False``) does not group on the host at all: the spans go
-to the device in arrival order and are grouped there by low trace id (the order of traces
-does not change a count), each range of days is one pass over the resident batch that skips
-the traces of other days (ZDL_DAYS_SKIP_OUTSIDE), and above 1024 services the context keeps
-one sparse sorted list with the day in the cell instead of a days x S x S table. Its days come
+Sorted output (``insertion_order=False``) uploads the batch once. With one range of days the
+spans go to the device in arrival order and are grouped there by low trace id (the order of
+traces does not change a count). When the days need several ranges (a context's cell index
+stays below 2^31: more than 21 days at 10 000 services), the batch is appended once to a
+device store (``zdl_store``) and each range links it from there through a host grouping
+permutation (``zdl_put_stored``: 4 B a span crosses PCIe per range, not the columns), skipping
+the traces of other days (ZDL_DAYS_SKIP_OUTSIDE). Above 1024 services the context keeps one
+sparse sorted list with the day in the cell instead of a days x S x S table. Its days come
 back ascending, each day's links sorted by (parent, child) names.
 """
 from __future__ import annotations
@@ -116,8 +119,18 @@ def _ranges(mids: List[int], max_days: int) -> List[List[int]]:
     return out
 
 
+def _group_perm(trace_lo: np.ndarray):
+    """GroupByTraceId's grouping as a permutation: spans of one low trace id together, in arrival
+    order inside the trace (a stable sort; the traces' own order does not change a count), and
+    the CSR offsets of the traces over it."""
+    perm = np.argsort(trace_lo, kind="stable")
+    lo = trace_lo[perm]
+    heads = np.flatnonzero(np.concatenate(([True], lo[1:] != lo[:-1]))) if len(lo) else np.zeros(0, np.int64)
+    return perm.astype(np.uint32), np.append(heads, len(lo)).astype(np.uint64)
+
+
 def _aggregate_sorted(spans: Sequence[Span], device: int) -> Dict[int, List[DependencyLink]]:
-    """aggregate_links(insertion_order=False): device grouping, one pass per range of days."""
+    """aggregate_links(insertion_order=False): the batch uploaded once, one pass per range of days."""
     svc, ip4, ip6 = Dictionary(), Dictionary(), Dictionary()
     cols = pack_traces([spans], svc, ip4, ip6)  # arrival order; trace_lo per span, grouped on the device
     cols.timestamp[:] = [guess_timestamp(s) for s in spans]
@@ -135,14 +148,22 @@ def _aggregate_sorted(spans: Sequence[Span], device: int) -> Dict[int, List[Depe
     names = svc.strings
     out: Dict[int, List[DependencyLink]] = {}
     ctx = N.Context(cap, device)
+    store = None
     try:
         ctx.set_ranks(N.ZDL_DICT_SERVICE, svc.ranks())
         ctx.set_ranks(N.ZDL_DICT_IPV4, ip4.ranks())
         ctx.set_ranks(N.ZDL_DICT_IPV6, ip6.ranks())
+        if len(rngs) > 1:  # several passes: the columns stay resident in a store
+            store = N.Store(device)
+            store.append(cols)
+            perm, offsets = _group_perm(cols.trace_lo)
         for rng in rngs:
             lo, hi = rng[0], rng[-1]
             ctx.set_days(lo, (hi - lo) // DAY_MS + 1, skip_outside=len(rngs) > 1)
-            ctx.put_spans_ungrouped(cols)
+            if store is None:
+                ctx.put_spans_ungrouped(cols)
+            else:
+                ctx.put_stored(store, perm, offsets)
             got_days, day, p, c, k, e = ctx.link_days(N.ZDL_ORDER_SORTED)
             for d in got_days:
                 out.setdefault(int(d), [])
@@ -150,6 +171,8 @@ def _aggregate_sorted(spans: Sequence[Span], device: int) -> Dict[int, List[Depe
                 out[int(d)].append(DependencyLink.create(names[a], names[b], int(x), int(y)))
     finally:
         ctx.close()
+        if store is not None:
+            store.close()
     return dict(sorted(out.items()))
 
 

@@ -20,9 +20,10 @@ returns the same links sorted by (parent, child) in String order.
 the logger enabled for DEBUG (java.util.logging FINE), every put takes the exact per-trace path
 with ZDL_FLAG_TREE_EXPORT and the device's reason codes (zdl_tree_reasons) are rendered as the
 reference's FINE messages, in its order (SpanNode.java:130, 145-147, 227-231;
-DependencyLinker.java:57-169). One difference: "processing <span>" and "found remote ancestor
-<span>" quote the node's first fragment in Trace.merge order, not the merged span (the same
-text whenever a node has one fragment).
+DependencyLinker.java:57-169). "processing <span>" and "found remote ancestor <span>" quote the
+node's span as Trace.merge leaves it (the fragments of its run merged, the trace id and a shared
+span's missing parent id filled in): `_merged_spans` replays Trace.merge's merge loop over the
+fragments in the device's sort order (zdl_tree_reasons), only to render that text.
 """
 from __future__ import annotations
 
@@ -53,6 +54,112 @@ def _capacity(n: int, window: bool = False) -> int:
     while cap < n:
         cap *= 2
     return cap
+
+
+class _EndpointTracker:
+    """Trace.EndpointTracker (Trace.java:131-155): whether fragments share one local endpoint."""
+    __slots__ = ("svc", "ip4", "ip6", "port")
+
+    def __init__(self):
+        self.svc = self.ip4 = self.ip6 = None
+        self.port = 0
+
+    def try_merge(self, e) -> bool:
+        if e is None:
+            return True
+        if self.svc is not None and e.service_name is not None and self.svc != e.service_name:
+            return False
+        if self.ip4 is not None and e.ipv4 is not None and self.ip4 != e.ipv4:
+            return False
+        if self.ip6 is not None and e.ipv6 is not None and self.ip6 != e.ipv6:
+            return False
+        if self.port != 0 and e.port != 0 and self.port != e.port:
+            return False
+        self.svc = self.svc if self.svc is not None else e.service_name
+        self.ip4 = self.ip4 if self.ip4 is not None else e.ipv4
+        self.ip6 = self.ip6 if self.ip6 is not None else e.ipv6
+        self.port = self.port or e.port
+        return True
+
+
+def _endpoint_merge(acc, src):
+    """Endpoint.Builder.merge (Endpoint.java:121-129); a put whose merge would dereference a null
+    source threw before anything was logged, so src is never needed as null here."""
+    if src is None:
+        return acc
+    return acc.__class__(acc.service_name if acc.service_name is not None else src.service_name,
+                         acc.ipv4 if acc.ipv4 is not None else src.ipv4,
+                         acc.ipv6 if acc.ipv6 is not None else src.ipv6, acc.port or src.port)
+
+
+def _span_merge(frags, trace_id):
+    """Span.Builder: frags[0].toBuilder() (trace id set), then merge(f) of every later fragment
+    in order (Span.java:358-388): fields the builder lacks, endpoints merged, annotations and tags
+    accumulated, the shared / debug flag bits OR-ed."""
+    from dataclasses import replace
+    first = frags[0]
+    d = {f: getattr(first, f) for f in first.__dataclass_fields__}
+    if len(first.trace_id) != len(trace_id):  # (Trace.java:47-49)
+        d["trace_id"] = trace_id
+    tags, anns = dict(first.tags), list(first.annotations)
+    sh_set, sh, db_set, db = first.shared is not None, bool(first.shared), first.debug is not None, bool(first.debug)
+    for src in frags[1:]:
+        for k in ("parent_id", "kind", "name"):
+            if d[k] is None:
+                d[k] = getattr(src, k)
+        for k in ("timestamp", "duration"):
+            if not d[k]:
+                d[k] = getattr(src, k)
+        for k in ("local_endpoint", "remote_endpoint"):
+            d[k] = getattr(src, k) if d[k] is None else _endpoint_merge(d[k], getattr(src, k))
+        anns.extend(src.annotations)
+        tags.update(dict(src.tags))
+        if src.shared is not None:
+            sh_set, sh = True, sh or bool(src.shared)
+        if src.debug is not None:
+            db_set, db = True, db or bool(src.debug)
+    d.update(tags=tuple(sorted(tags.items())), annotations=tuple(sorted(set(anns))),
+             shared=sh if sh_set else None, debug=db if db_set else None)
+    if d["parent_id"] == d["id"]:
+        d["parent_id"] = None
+    return replace(first, **d)
+
+
+def _merged_spans(spans, pos, trace_id):
+    """Trace.merge's output spans (Trace.java:42-84) keyed by their first fragment's index in
+    `spans`: the merge loop over the spans in the device's sort order `pos` (Trace.merge's
+    CLEANUP_COMPARATOR order, from zdl_tree_reasons): a run of one id and sharedness whose local
+    endpoints agree (EndpointTracker) is one span; a shared span without a parent id that
+    follows a fragment with one takes that fragment's (:76-79); a span whose trace id is not
+    the trace's longest takes it."""
+    order = sorted(range(len(spans)), key=lambda i: pos[i])
+    res = [spans[i] for i in order]
+    out = {}
+    n, k = len(order), 0
+    while k < n:
+        k0, prev = k, res[k]
+        prev_shared = prev.shared is True
+        frags = [prev]
+        tracker = None
+        while k + 1 < n:
+            nxt = res[k + 1]
+            if nxt.id != res[k0].id:
+                break
+            if tracker is None:
+                tracker = _EndpointTracker()
+                tracker.try_merge(prev.local_endpoint)
+            if prev_shared == (nxt.shared is True) and tracker.try_merge(nxt.local_endpoint):
+                frags.append(nxt)
+                prev = nxt
+                k += 1
+                continue
+            if nxt.shared is True and nxt.parent_id is None and prev.parent_id is not None:
+                res[k + 1] = nxt.to_builder(parent_id=prev.parent_id)
+            break
+        out[order[k0]] = frags[0] if len(frags) == 1 and len(frags[0].trace_id) == len(trace_id) \
+            else _span_merge(frags, trace_id)
+        k += 1
+    return out
 
 
 class DependencyLinker:
@@ -153,11 +260,13 @@ class DependencyLinker:
                          % (cleaned_tid(i), flat[roots[0]].id, flat[i].id))
             if not roots:
                 fine(f"substituting dummy node for missing root span: traceId={root_tid}")
+            merged = _merged_spans(t, [srt[i] for i in idx], tid)  # by local index
+            quote = lambda i: merged[i - base].to_json_v2()  # noqa: E731
             fine("traversing trace tree, breadth-first")
             if not roots:
                 fine("skipping fake root node for broken span tree")
             for i in sorted((i for i in heads if bfs[i] >= 0), key=lambda i: bfs[i]):
-                fine(f"processing {flat[i].to_json_v2()}")
+                fine(f"processing {quote(i)}")
                 r = int(reason[i])
                 code = r & 7
                 pa, ch, xpa, xch = (int(x) for x in link[i])
@@ -172,7 +281,7 @@ class DependencyLinker:
                     fine(f"incrementing {err}link {names[pa]} -> {names[ch]}")
                 elif code in (N.ZDL_RSN_LINK, N.ZDL_RSN_NO_REMOTE_ANCESTOR):
                     if r & N.ZDL_RSN_ANCESTOR:
-                        fine(f"found remote ancestor {flat[anc[i]].to_json_v2()}")
+                        fine(f"found remote ancestor {quote(int(anc[i]))}")
                     if r & N.ZDL_RSN_MISSING_LINK:
                         fine("detected missing link to client span")
                         fine(f"incrementing link {names[xpa]} -> {names[xch]}")

@@ -106,6 +106,12 @@ def _synth() -> C.CDLL:
         L.zdl_synth_sizes.argtypes = [C.POINTER(Params), C.c_void_p, C.c_int]
         L.zdl_synth_fill.restype = None
         L.zdl_synth_fill.argtypes = [C.POINTER(Params), C.c_void_p] + [C.c_void_p] * 9 + [C.c_int]
+        L.zdl_synth_shard_plan.restype = None
+        L.zdl_synth_shard_plan.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_uint32, C.c_int,
+                                           C.c_void_p, C.c_void_p]
+        L.zdl_synth_shard.restype = C.c_double
+        L.zdl_synth_shard.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_uint32, C.c_int,
+                                      C.c_void_p, C.c_void_p]
         _lib = L
     return _lib
 
@@ -225,3 +231,38 @@ def spans_of(cols: Columns, w: "Workload", n_traces: int):
                            (("error", ""),) if pf & _PF_ERROR else (), None if sh == 0 else sh == 2, None))
         out.append(tr)
     return out
+
+
+def shard_host(cols: Columns, n_shards: int, threads: int = 0, grouped: bool = True, timestamps: bool = True):
+    """A device group's host split (zipkin_amd/csrc/zdl_shard.h, the code libzdl's group_put
+    runs) over host columns: (shards as Columns, seconds of plan + scatter). grouped=False
+    shards span by span (ungrouped input; the shards' offsets are then empty). timestamps=False
+    splits the 44 B/span a put without a time window passes (the shards' timestamp columns are
+    then empty)."""
+    from ._native import SpanCols
+    threads = threads or min(16, os.cpu_count() or 1)
+    L = _synth()
+    ptr = lambda a: a.ctypes.data if a is not None else None  # noqa: E731
+    src = SpanCols(ptr(cols.trace_lo), ptr(cols.id), ptr(cols.parent_id), ptr(cols.local_svc), ptr(cols.remote_svc),
+                   ptr(cols.local_ip4), ptr(cols.local_ip6), ptr(cols.port_flags),
+                   ptr(cols.timestamp) if timestamps else None, None)
+    off = cols.offsets if grouped else None
+    nt = cols.n_traces if grouped else 0
+    spans = np.zeros(n_shards, np.uint64)
+    traces = np.zeros(n_shards, np.uint64)
+    L.zdl_synth_shard_plan(C.addressof(src), cols.n_spans, ptr(off), nt, n_shards, threads, ptr(spans), ptr(traces))
+    out = []
+    for d in range(n_shards):
+        n = int(spans[d])
+        out.append(Columns(np.empty(n, np.uint64), np.empty(n, np.uint64), np.empty(n, np.uint64),
+                           np.empty(n, np.int32), np.empty(n, np.int32), np.empty(n, np.int32), np.empty(n, np.int32),
+                           np.empty(n, np.uint32), np.empty(n if timestamps else 0, np.int64),
+                           np.zeros(int(traces[d]) + 1 if grouped else 1, np.uint64)))
+    dst = (SpanCols * n_shards)(*[SpanCols(ptr(o.trace_lo), ptr(o.id), ptr(o.parent_id), ptr(o.local_svc),
+                                           ptr(o.remote_svc), ptr(o.local_ip4), ptr(o.local_ip6), ptr(o.port_flags),
+                                           ptr(o.timestamp) if timestamps else None, None) for o in out])
+    offp = (C.c_void_p * n_shards)(*[ptr(o.offsets) for o in out])
+    sec = float(L.zdl_synth_shard(C.addressof(src), cols.n_spans, ptr(off), nt, n_shards, threads,
+                                  C.addressof(dst), C.addressof(offp)))
+    return out, sec
+
