@@ -94,8 +94,8 @@ extern "C" {
 #define ZDL_FLAG_TIMING_ALL 2u   /* record HIP events around every kernel (all zdl_kernel_times fields) */
 #define ZDL_FLAG_INSERTION_ORDER 4u  /* keep, per (parent, child), the rank of its first addLink so that
                                         zdl_link can return ZDL_ORDER_INSERTION; puts take the exact
-                                        per-trace path (slower than the default streaming path); traces
-                                        are limited to 2^21 spans */
+                                        per-trace path (slower than the default streaming path); any
+                                        trace size */
 #define ZDL_FLAG_DENSE_TABLE 16u     /* keep the S x S count table above 1024 services (a device group's
                                         and a multi-process job's RCCL reduce sums those tables); without
                                         it such a context keeps its links as one sorted list instead

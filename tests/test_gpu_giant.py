@@ -87,6 +87,23 @@ def test_c5_giants_tiers_vs_cpp(gmin, monkeypatch):
     assert _link(cols, 10_000) == _oracle(cols)
 
 
+def test_giants_beyond_a_million_spans_vs_cpp():
+    """Traces of 1.5M and 3M spans (beyond round 5's 2^20-span tier limit; the tier now takes up
+    to 2^22 spans, 4096 tiles and buckets) are linked by the whole GPU: bit-exact vs the
+    restatement, and the tier (not k_tail's one workgroup) ran them."""
+    parts = [_giant(50, 1_500_000), _slice(synth.generate(synth.C5.scaled(20_000)), 0, 20_000), _giant(51, 3_000_000)]
+    cols = concat_columns(parts)
+    sizes = np.diff(cols.offsets.astype(np.int64))
+    assert sizes.max() >= 2_900_000 and (sizes > (1 << 20)).sum() == 2
+    ctx = N.Context(10_000, timing_all=True)
+    ctx.put_spans(cols)
+    got = sorted(_tuples(*ctx.link()))
+    kt = ctx.kernel_times()
+    ctx.close()
+    assert got == _oracle(cols)
+    assert kt.giant_ms > 0
+
+
 def test_c5_giants_window_vs_cpp(monkeypatch):
     """The window filters whole traces by QueryRequest.test's rule (first parentless span's
     timestamp, else the smallest); giants are stamped at different times so some fall out."""

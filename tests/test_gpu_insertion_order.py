@@ -133,6 +133,39 @@ def test_big_traces_order_vs_cpp_oracle():
     _ordered_vs_cpp(cols, 64, svc_rank=svc.ranks(), ip4_rank=ip4.ranks(), ip6_rank=ip6.ranks())
 
 
+def test_trace_beyond_2_21_spans_order_vs_cpp_oracle():
+    """One trace of 2^21 + 1 spans between small ones (round 5 refused traces of 2^21 - 1 spans
+    or more: big_bfs packed its sort keys in 21-bit fields, the ranks in 24): the breadth-first
+    order comes from wide keys, the ranks are (position + index) << 1 | k."""
+    from zipkin_amd.columnar import concat_columns
+    huge = synth.generate(synth.Workload("huge", 0x5EED0A21, 1, 50, max_depth=64, size_dist=2,
+                                         max_size=(1 << 21) + 1, max_fanout=1000))
+    assert huge.n_spans == (1 << 21) + 1
+    small = synth.generate(synth.C2.scaled(20_000))
+    cols = concat_columns([_first(small, 10_000), huge, _rest(small, 10_000)])
+    assert len(_ordered_vs_cpp(cols, 64)) > 100
+
+
+def _first(cols, k):
+    return next(_split_at(cols, k))
+
+
+def _rest(cols, k):
+    it = _split_at(cols, k)
+    next(it)
+    return next(it)
+
+
+def _split_at(cols, k):
+    off = cols.offsets.astype(np.int64)
+    f = ("trace_lo", "id", "parent_id", "local_svc", "remote_svc", "local_ip4", "local_ip6", "port_flags",
+         "timestamp")
+    for a, b in ((0, k), (k, cols.n_traces)):
+        s0, s1 = off[a], off[b]
+        yield Columns(*(np.ascontiguousarray(getattr(cols, n)[s0:s1]) for n in f),
+                      (off[a:b + 1] - s0).astype(np.uint64))
+
+
 @pytest.mark.parametrize("n_services", [64, 300])
 def test_c2_order_vs_cpp_oracle(n_services):
     w = synth.C2.scaled(100_000)

@@ -191,7 +191,7 @@ static void check_ord(std::mt19937_64& r, int W) {
     for (uint32_t c = 0; c < S * S; ++c)
       if (r() % 3 == 0) {
         const uint64_t pos = r() % ORD_POS_LIMIT, bfs = r() % 1000, kk = r() % 2;
-        first[k][c] = (pos << 24) | (bfs << 1) | kk;  // ord_rank's layout
+        first[k][c] = ((pos + bfs) << 1) | kk;  // ord_rank's layout
         v.push_back({first[k][c], c});
       }
     std::sort(v.begin(), v.end());

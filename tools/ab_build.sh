@@ -3,7 +3,7 @@
 # (pairs of arguments); each lands in ab/NAME/libzdl.so (ZDL_LIB_PATH selects it). One object per
 # source, compiled in parallel (as __graft_entry__.build does), then one link per variant.
 cd "$(dirname "$0")/.."
-C=zipkin_amd/csrc
+C=${ZDL_AB_SRC:-zipkin_amd/csrc}
 SRCS="zdl zdl_group zdl_sparse zdl_proto3 zdl_rows zdl_store"
 while [ $# -ge 2 ]; do
   n=$1; d=$2; shift 2

@@ -59,24 +59,15 @@ constexpr int wdense_max(int window) { return window ? WDENSE_MAX_WINDOW : WDENS
 constexpr int wtable_bytes(int window) { return window ? WTABLE_BYTES_WINDOW : WTABLE_BYTES; }
 // LOG mode (WDENSE_MAX < S*S <= PMAX << PSHIFT, e.g. C3's 500 services): k_link appends every
 // link to a per-wave log in HBM and counts it per partition of 2^PSHIFT cells; k_pscan /
-// k_scatter group the log by partition, k_hist counts each partition in a dense LDS table.
-constexpr int PSHIFT = 12;          // cells per partition: 4096 u64 LDS cells = 32 KB in k_hist
-constexpr int PMAX = 256;           // partitions (per-wave LDS counters in k_link): S <= 1024
-// ZDL_LOG_ROWS (round 5; 0 = round 4's reduce, for A/B builds): k_link writes ONE partition-count
-// row per workgroup (its waves summed in LDS), k_scatter2 takes one k_link workgroup's segments
-// in order - so a partition's entries of consecutive segments land in ONE contiguous run (the
-// prefix runs over 512 rows instead of 8192 waves) - and ranks a wave's entries per partition by
-// ballot masks (one LDS atomic per partition a wave holds, not one per entry); k_hist2 runs one
-// 1024-thread workgroup per CU (fewer flushes of each partition's cells).
-#ifndef ZDL_LOG_ROWS
-#define ZDL_LOG_ROWS 1
-#endif
-#ifndef ZDL_LOG_ROW_WAVES
-#define ZDL_LOG_ROW_WAVES 4  // k_link waves summed into one row (a divisor of 12 and 16)
-#endif
-#ifndef ZDL_SCATTER_PEERS
-#define ZDL_SCATTER_PEERS 0  // k_scatter2 ranks by ballot masks (1) or by an LDS atomic per entry (0)
-#endif
+// k_scatter2 group the log by partition, k_hist2 counts each partition in dense LDS tables.
+constexpr int PSHIFT = 12;          // cells per partition: 4096 u32 call + error cells in k_hist2
+constexpr int PMAX = 256;           // partitions (k_link's LDS counters per row): S <= 1024
+// Rows (round 5): k_link's waves count their log entries per partition in one LDS counter
+// array per row of ZDL_LOG_ROW_WAVES waves (round 6: shared by the row's waves, which leaves
+// the hot corner 12-14 KB more), k_scatter2 takes one row's segments in order - so a
+// partition's entries of consecutive segments land in ONE contiguous run - and k_hist2 runs
+// one 1024-thread workgroup per CU (fewer flushes of each partition's cells).
+constexpr int ZDL_LOG_ROW_WAVES = 4;  // a divisor of 12 and 16
 // k_link's table modes (template parameter DENSE): hash, dense, log
 constexpr int TM_HASH = 0, TM_DENSE = 1, TM_LOG = 2;
 // SORT (sparse contexts, zdl_sparse.h): k_link logs every link like LOG, without partition
@@ -163,6 +154,7 @@ struct Args {
   uint32_t* o_fa;
   uint32_t* o_fb;
   uint32_t* o_bfs;
+  uint32_t* o_pay;  // big_bfs's payload for traces of 2^21 - 1 spans and more (null when none)
   // LOG mode: wave gw's log segment starts at lg + lg_start[gw] (= 2 * its first span) and
   // holds lg_n[gw] entries (cell << 1 | error); lg_cnt[gw * lg_P + p] = its entries in
   // partition p (cell >> PSHIFT); lg_P partitions, lg_W = k_link's waves
@@ -219,7 +211,7 @@ constexpr unsigned long long FLAG_TAIL = 1ull << 62;  // lazy put: k_mid / k_tai
 __device__ void lk_lazy_end(const Args& A, uint32_t* scratch);  // k_link's end in a lazy put (below)
 __device__ void lk_lazy_end_log(const Args& A, uint32_t* scratch);  // ... of a LOG-mode put
 #include "zdl_link.inc"  // k_link, full_windows (need zdl_full.inc's helpers)
-#include "zdl_log.inc"   // LOG mode reduce: k_pscan, k_scatter, k_hist
+#include "zdl_log.inc"   // LOG mode reduce: k_pscan, k_pbase, k_scatter2, k_hist2
 
 // ---------------------------------------------------------- big traces (k_tail)
 // k_tail's second part: one workgroup per trace longer than WSMALL; arrays live in HBM
@@ -271,9 +263,14 @@ __device__ __forceinline__ uint32_t big_lower(const unsigned long long* key, uin
 // nodes sorted by (parent, spanToParent entry position) - see wave_bfs for the entry
 // rule; the synthetic root is position n. Then level by level: a frontier in
 // breadth-first order, each node's children appended at a scanned offset.
+// Sort keys: (parent, entry, node) in 21 bits each while n < 2^21 - 1; a longer trace sorts
+// (parent << 32 | entry) keys with the node as a payload in pay[] (a live node's (parent,
+// entry) is unique, so the payload needs no ordering of its own).
 __device__ __forceinline__ void big_bfs(const View& v, int n, int rp, unsigned long long* key, uint32_t* fa,
-                                        uint32_t* fb, uint32_t* bfs) {
+                                        uint32_t* fb, uint32_t* bfs, uint32_t* pay) {
   constexpr unsigned long long M21 = (1ull << 21) - 1;
+  const bool wide = n >= (1 << 21) - 1;
+  const int psh = wide ? 32 : 42;
   for (int p = threadIdx.x; p < n; p += BIG_WG) {
     unsigned long long k = ~0ull;
     const int par = v.parent[p];
@@ -295,9 +292,10 @@ __device__ __forceinline__ void big_bfs(const View& v, int n, int rp, unsigned l
           if (v.live[q] && !is_shared(v.pf[v.perm[q]])) { ek = q; break; }
       }
       const unsigned long long pp = par >= 0 ? (unsigned long long)par : (unsigned long long)n;
-      k = (pp << 42) | ((unsigned long long)ek << 21) | (unsigned long long)p;
+      k = wide ? (pp << 32) | (unsigned long long)ek : (pp << 42) | ((unsigned long long)ek << 21) | (unsigned long long)p;
     }
     key[p] = k;
+    if (wide) pay[p] = (uint32_t)p;
   }
   big_sync();
   int npad = 1;
@@ -308,7 +306,15 @@ __device__ __forceinline__ void big_bfs(const View& v, int n, int rp, unsigned l
         const int l = i ^ jj;
         if (l > i && l < n) {
           const unsigned long long a = key[i], b = key[l];
-          if (b < a) { key[i] = b; key[l] = a; }
+          if (b < a) {
+            key[i] = b;
+            key[l] = a;
+            if (wide) {
+              const uint32_t t = pay[i];
+              pay[i] = pay[l];
+              pay[l] = t;
+            }
+          }
         }
       }
       big_sync();
@@ -329,13 +335,13 @@ __device__ __forceinline__ void big_bfs(const View& v, int n, int rp, unsigned l
       uint32_t lo = 0, cnt = 0;
       if (i < fsz) {
         const unsigned long long u = fa[i];
-        lo = big_lower(key, (uint32_t)n, u << 42);
-        cnt = big_lower(key, (uint32_t)n, (u + 1) << 42) - lo;
+        lo = big_lower(key, (uint32_t)n, u << psh);
+        cnt = big_lower(key, (uint32_t)n, (u + 1) << psh) - lo;
       }
       uint32_t tot;
       const uint32_t o = gsz + big_scan(cnt, &tot);
       for (uint32_t j = 0; j < cnt; ++j) {
-        const uint32_t node = (uint32_t)(key[lo + j] & M21);
+        const uint32_t node = wide ? pay[lo + j] : (uint32_t)(key[lo + j] & M21);
         fb[o + j] = node;
         bfs[node] = next + o + j;
       }
@@ -1002,13 +1008,8 @@ __device__ __forceinline__ void big_exact(const Args& A, uint64_t b, int n, uint
   big_sync();
   uint32_t* bfs = nullptr;
   if (ORD) {
-    if (n >= (1 << 21) - 1) {  // ranks pack positions in 21 bits
-      if (threadIdx.x == 0) atomicOr(A.status, ST_ORDLIM);
-      big_sync();
-      return;
-    }
     bfs = A.o_bfs + b;
-    big_bfs(v, n, rp, A.o_key + b, A.o_fa + b, A.o_fb + b, bfs);
+    big_bfs(v, n, rp, A.o_key + b, A.o_fa + b, A.o_fb + b, bfs, A.o_pay ? A.o_pay + b : nullptr);
     big_sync();
   }
   if (A.tr_parent) {  // ZDL_FLAG_TREE_EXPORT / _STREAM (wave_tree_export's encoding)
@@ -1643,7 +1644,7 @@ struct zdl_ctx {
   DevBuf<uint32_t> ord_cnt;
 
   uint64_t span_base = 0;
-  DevBuf<uint32_t> o_fa, o_fb, o_bfs;
+  DevBuf<uint32_t> o_fa, o_fb, o_bfs, o_pay;
   // per-put scratch
   DevBuf<uint32_t> big_list, counters;
   DevBuf<uint32_t> big_exact_list;  // k_big -> k_tail: the back-list traces for the exact path
@@ -1825,7 +1826,6 @@ int status_code(zdl_ctx* c, uint32_t st) {
   if (st & ST_BADSVC) return fail(c, ZDL_EINVAL, "service id >= n_services");
   if (st & ST_BADOFF) return fail(c, ZDL_EINVAL, "trace offsets are not non-decreasing");
   if (st & ST_INTERNAL) return fail(c, ZDL_EDEVICE, "internal consistency check failed on the device");
-  if (st & ST_ORDLIM) return fail(c, ZDL_EINVAL, "insertion order: a trace has more than 2^21 - 2 spans");
   if (st & ST_DAYS) return fail(c, ZDL_EINVAL, "daily buckets: a trace has no timestamp or its day is outside the range");
   return ZDL_OK;
 }
@@ -2078,7 +2078,7 @@ void zdl_destroy(zdl_ctx* c) {
   for (auto& r : c->rank) r.release();
   c->call.release(); c->errc.release(); c->status.release();
   c->first.release(); c->ord_n.release(); c->ord_w.release(); c->ord_log.release(); c->ord_part.release();
-  c->ord_start.release(); c->ord_cnt.release(); c->day_first.release(); c->o_key.release(); c->o_fa.release(); c->o_fb.release(); c->o_bfs.release();
+  c->ord_start.release(); c->ord_cnt.release(); c->day_first.release(); c->o_key.release(); c->o_fa.release(); c->o_fb.release(); c->o_bfs.release(); c->o_pay.release();
   c->big_list.release(); c->big_stat.release(); c->big_exact_list.release(); c->counters.release(); c->retry.release();
   c->cx_win.release();
   if (c->prof_on && c->prof.p) {
@@ -2755,6 +2755,7 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
     HIP_TRY(c, c->o_fa.ensure(n_spans));
     HIP_TRY(c, c->o_fb.ensure(n_spans));
     HIP_TRY(c, c->o_bfs.ensure(n_spans));
+    if (n_spans >= (1u << 21) - 1) HIP_TRY(c, c->o_pay.ensure(n_spans));  // a trace may need big_bfs's wide keys
     A.first = c->first.p;
     A.ord_w = c->ord_w.p;
     A.span_base = c->span_base;
@@ -2762,6 +2763,7 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
     A.o_fa = c->o_fa.p;
     A.o_fb = c->o_fb.p;
     A.o_bfs = c->o_bfs.p;
+    A.o_pay = n_spans >= (1u << 21) - 1 ? c->o_pay.p : nullptr;
   }
   const bool ordered = SS <= (size_t)COMPACT_WG * 8 && !c->ord && !c->days && !c->sparse;
   static const bool nolazy = getenv("ZDL_NOLAZY") != nullptr;
@@ -2792,8 +2794,7 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   c->last_log_lP = tm == TM_LOG ? lP : 0u;
   c->last_sparse_E = 0;
   if (tm == TM_LOG) {  // group the log by partition, count each partition in LDS (zdl_log.inc)
-#if ZDL_LOG_ROWS
-    // rows = k_link's workgroups (the column prefix over 512 rows), a scatter workgroup per row
+    // rows of ZDL_LOG_ROW_WAVES k_link waves, a scatter workgroup per row
     const uint32_t rows = lW / ZDL_LOG_ROW_WAVES;
     hipLaunchKernelGGL(k_pscan, dim3(lP), dim3(PSCAN_WG), 0, c->stream, c->lg_cnt.p, rows, lP, c->lg_tot.p);
     hipLaunchKernelGGL(k_pbase, dim3(1), dim3(PMAX), 0, c->stream, c->lg_tot.p, lP, c->lg_tot.p + PMAX);
@@ -2801,15 +2802,6 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
                        c->lg_n.p, c->lg_cnt.p, (uint32_t)ZDL_LOG_ROW_WAVES, lP, c->lg_tot.p + PMAX, c->lg_grp.p);
     hipLaunchKernelGGL(k_hist2, dim3((unsigned)c->cus), dim3(HIST2_WG), 0, c->stream, c->lg_grp.p,
                        c->lg_tot.p + PMAX, lP, (uint64_t)SS, c->call.p, c->errc.p);
-#else
-    hipLaunchKernelGGL(k_pscan, dim3(lP), dim3(PSCAN_WG), 0, c->stream, c->lg_cnt.p, lW, lP, c->lg_tot.p);
-    hipLaunchKernelGGL(k_pbase, dim3(1), dim3(PMAX), 0, c->stream, c->lg_tot.p, lP, c->lg_tot.p + PMAX);
-    hipLaunchKernelGGL(k_scatter, dim3((unsigned)std::min<uint32_t>(lW, (uint32_t)c->cus * 8)), dim3(SCATTER_WG), 0,
-                       c->stream, c->lg.p, c->lg_start.p, c->lg_n.p, c->lg_cnt.p, lW, lP, c->lg_tot.p + PMAX,
-                       c->lg_grp.p);
-    hipLaunchKernelGGL(k_hist, dim3((unsigned)c->cus * 4), dim3(HIST_WG), 0, c->stream, c->lg_grp.p,
-                       c->lg_tot.p + PMAX, lP, (uint64_t)SS, c->call.p, c->errc.p);
-#endif
     const hipError_t ke = hipGetLastError();
     if (ke != hipSuccess) {
       c->poisoned = true;
@@ -4228,9 +4220,9 @@ int zdl_add_links(zdl_ctx* c, const int32_t* parent, const int32_t* child, const
   HIP_TRY(c, hipMemcpyAsync(c->mi_err.p, error_count, n * 8, hipMemcpyHostToDevice, s));
   hipLaunchKernelGGL(k_merge_accum, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, c->mi_p.p, c->mi_c.p,
                      c->mi_call.p, c->mi_err.p, n, c->S, c->call.p, c->errc.p,
-                     c->ord ? c->first.p : c->m_first.p, c->status.p, c->ord ? c->span_base : 0, c->ord ? 24 : 0);
+                     c->ord ? c->first.p : c->m_first.p, c->status.p, c->ord ? c->span_base : 0, c->ord ? 1 : 0);
   HIP_TRY(c, hipGetLastError());
-  if (c->ord) c->span_base += n;  // the links rank before anything put afterwards
+  if (c->ord) c->span_base += n;  // the links rank before anything put afterwards (ord_rank's layout)
   c->map_fresh = false;
   return zdl_sync(c);
 }
@@ -4593,7 +4585,7 @@ static int comm_sum_ord(zdl_ctx* c) {
                        (uint64_t)SS, c->comm_rank);
   } else {
     if (c->span_base >= zdl_xplan::ORD_POS_LIMIT)
-      return fail(c, ZDL_EINVAL, "insertion order across ranks: more than 2^34 spans put on this rank");
+      return fail(c, ZDL_EINVAL, "insertion order across ranks: more than 2^56 spans put on this rank");
     hipLaunchKernelGGL(k_ord_tag, dim3(g), dim3(256), 0, c->stream, c->first.p, c->red_first.p, (uint64_t)SS,
                        c->comm_rank);
   }

@@ -21,7 +21,7 @@
 
 namespace zdl {
 
-enum : uint32_t { ST_NPE = 1u, ST_BADSVC = 2u, ST_BADOFF = 4u, ST_IAE = 8u, ST_INTERNAL = 16u, ST_ORDLIM = 32u, ST_DAYS = 64u };
+enum : uint32_t { ST_NPE = 1u, ST_BADSVC = 2u, ST_BADOFF = 4u, ST_IAE = 8u, ST_INTERNAL = 16u, ST_DAYS = 64u };  // (32: unused)
 enum : int32_t { PAR_TERMINAL = -1, PAR_NONMEMBER = -3 };
 
 template <class PermT, class ParT>
@@ -435,14 +435,17 @@ __device__ __forceinline__ Rsn node_reason(uint32_t pf, bool haschild, int32_t s
 }
 
 // Insertion order (ZDL_FLAG_INSERTION_ORDER): first[cell] keeps the smallest rank of an
-// addLink of that (parent, child): (put-global position of the trace's first span) << 24
-// | (breadth-first index of the node << 1 | k). The plain load skips the atomic once a
-// smaller rank is in (ranks only decrease; a stale read only costs the atomic).
+// addLink of that (parent, child): (put-global position of the trace's first span + the
+// node's breadth-first index) << 1 | k. A trace of n spans has fewer than n nodes, so its
+// ranks lie below the next trace's first position: the order is (trace, breadth-first
+// index, k) with no bit field to outgrow - any trace size, positions below 2^62. The plain
+// load skips the atomic once a smaller rank is in (ranks only decrease; a stale read only
+// costs the atomic).
 __device__ __forceinline__ void ord_min(unsigned long long* f, unsigned long long rank) {
   if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > rank) atomicMin(f, rank);
 }
 __device__ __forceinline__ unsigned long long ord_rank(uint64_t trace_pos, uint32_t bfs, int k) {
-  return ((unsigned long long)trace_pos << 24) | ((unsigned long long)bfs << 1) | (unsigned long long)k;
+  return (((unsigned long long)trace_pos + bfs) << 1) | (unsigned long long)k;
 }
 
 // Daily buckets (ITDependencies.aggregateLinks, ITDependencies.java:666-700): a trace's day

@@ -12,7 +12,7 @@
 // 2. Insertion order across the ranks of a job: the job's list is DependencyLinker.merge over
 //    the ranks' link() lists concatenated in rank order (DependencyLinker.java:189-204: a
 //    LinkedHashMap keyed by (parent, child), so a pair sits where it is first seen). Each rank's
-//    first-seen rank of a pair (ord_rank: put position << 24 | breadth-first index << 1 | k) is
+//    first-seen rank of a pair (ord_rank: (put position + breadth-first index) << 1 | k) is
 //    tagged with the rank number above it, and one element-wise MIN over the ranks (ncclMin,
 //    next to the sums) gives every pair its first rank in the concatenation.
 #pragma once
@@ -30,10 +30,11 @@
 
 namespace zdl_xplan {
 
-// Rank tags: ord ranks stay below 2^58 (span positions below 2^34, ORD_POS_LIMIT) so that 6
-// bits of job rank fit above them; an empty cell (~0) stays the largest value.
+// Rank tags: ord ranks ((position + breadth-first index) << 1 | k) stay below 2^58 (span
+// positions below 2^56, ORD_POS_LIMIT) so that 6 bits of job rank fit above them; an empty cell
+// (~0) stays the largest value.
 constexpr int ORD_TAG_SHIFT = 58;
-constexpr uint64_t ORD_POS_LIMIT = 1ull << 34;
+constexpr uint64_t ORD_POS_LIMIT = 1ull << 56;
 constexpr int ORD_MAX_WORLD = 64;
 ZDL_XPLAN_HD inline uint64_t ord_tag(uint64_t first, int rank) {
   return first == ~0ull ? first : (first | ((uint64_t)rank << ORD_TAG_SHIFT));
