@@ -1007,7 +1007,6 @@ def main():
                               "the log read once (4 B/entry); the kernels move 12 B/entry (scatter reads "
                               "and writes it, hist reads it) plus the per-row partition counts"}
     ctxs = []
-    del keep, batches[1:]
     if dist:
         tt = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -1026,31 +1025,54 @@ def main():
     side = world == 1 and config == "c2"  # the side legs run on C2 only
     if side and not args.no_insertion_order:
         # the DependencyLinker facade's engine configuration: its table capacity for S services
-        # (_capacity: the dense LDS table up to 67) on an insertion-order context, service ranks set
+        # (_capacity: the dense LDS table up to 67) on an insertion-order context, service ranks set;
+        # two contexts in flight as in the headline (a caller linking consecutive batches), and
+        # the same steps one at a time on one context (as the Python facade drives it)
         from zipkin_amd.linker import _capacity
-        ictx = N.Context(_capacity(S), device=local, insertion_order=True)
         names_w = synth.service_names(w)
         rk = np.empty(S, np.int32)
         rk[np.argsort(np.array(names_w, dtype=object), kind="stable")] = np.arange(S, dtype=np.int32)
-        ictx.set_ranks(N.ZDL_DICT_SERVICE, rk)
+        ictxs = [N.Context(_capacity(S), device=local, insertion_order=True) for _ in range(2)]
+        for ic in ictxs:
+            ic.set_ranks(N.ZDL_DICT_SERVICE, rk)
 
-        def istep():
-            ictx.reset()
-            ictx.put_spans_device(ptrs, cols.n_spans, doff.data_ptr(), cols.n_traces)
-            return ictx.link(N.ZDL_ORDER_INSERTION)
+        def iput(ic, j):
+            bp, bo = batches[j] if j < len(batches) else batches[0]
+            ic.reset()
+            ic.put_spans_device(bp, cols.n_spans, bo.data_ptr(), cols.n_traces)
 
-        istep()
-        ictx.sync()
-        ik = 3
+        def irun(k_steps, inflight_i):
+            res = None
+            for k in range(k_steps):
+                iput(ictxs[k % inflight_i], k % inflight_i)
+                if k >= inflight_i - 1:
+                    res = ictxs[(k - inflight_i + 1) % inflight_i].link(N.ZDL_ORDER_INSERTION)
+            for k in range(max(k_steps - inflight_i + 1, 0), k_steps):
+                res = ictxs[k % inflight_i].link(N.ZDL_ORDER_INSERTION)
+            return res
+
+        irun(3, 2)
+        for ic in ictxs:
+            ic.sync()
+        ik = max(args.steps, 10)
         t1 = time.perf_counter()
-        for _ in range(ik):
-            ins_out = istep()
-        ictx.sync()
+        ins_out = irun(ik, 2)
+        for ic in ictxs:
+            ic.sync()
         it = (time.perf_counter() - t1) / ik
-        ictx.close()
-        ins = {"ms_per_step": it * 1e3, "spans_per_s": cols.n_spans / it, "steps": ik, "parity": None,
+        t1 = time.perf_counter()
+        irun(ik, 1)
+        ictxs[0].sync()
+        it1 = (time.perf_counter() - t1) / ik
+        for ic in ictxs:
+            ic.close()
+        ins = {"ms_per_step": it * 1e3, "spans_per_s": cols.n_spans / it, "steps": ik, "inflight": 2,
+               "ms_per_step_serial": it1 * 1e3, "parity": None,
                "capacity": _capacity(S), "note": "DependencyLinker facade's context: _capacity(S) services, "
-                                                 "insertion order, service ranks; link(ZDL_ORDER_INSERTION)"}
+                                                 "insertion order, service ranks; reset + put + link(ZDL_ORDER_"
+                                                 "INSERTION) per step, two contexts in flight like the headline "
+                                                 "(serial: one context, one step at a time)"}
+    del keep, batches[1:]  # (the insertion-order leg's second context read its own copy, as the headline's)
     # side measurement (not `value`): the same batch as a proto3 ListOfSpans decoded on the device
     # (zdl_decode_proto3) and linked from the decoded HBM columns
     p3 = None
@@ -1125,7 +1147,8 @@ def main():
             iseq = list(zip(ip.tolist(), ic.tolist(), inn.tolist(), ie.tolist()))
             oseq = list(zip(op.tolist(), oc.tolist(), on.tolist(), oe.tolist()))
             ins["parity"] = "exact order" if (st == 0 and iseq == oseq) else "MISMATCH"
-            log(f"insertion order: {ins['ms_per_step']:.2f} ms/step, {ins['parity']}")
+            log(f"insertion order: {ins['ms_per_step']:.3f} ms/step in flight ({ins['ms_per_step_serial']:.3f} serial), "
+                f"{ins['parity']}")
         log(f"parity vs C++ restatement ({threads} threads, {t_multi:.2f}s): {parity}, {len(got)} links")
         if not args.no_cpu_baseline:
             # the whole batch on one thread = one DependencyLinker over every trace
