@@ -62,6 +62,7 @@ constexpr int wtable_bytes(int window) { return window ? WTABLE_BYTES_WINDOW : W
 // k_scatter2 group the log by partition, k_hist2 counts each partition in dense LDS tables.
 constexpr int PSHIFT = 12;          // cells per partition: 4096 u32 call + error cells in k_hist2
 constexpr int PMAX = 256;           // partitions (k_link's LDS counters per row): S <= 1024
+constexpr uint32_t LBLK = 1024;     // entries per block of LOG mode's block pool
 // Rows (round 5): k_link's waves count their log entries per partition in one LDS counter
 // array per row of ZDL_LOG_ROW_WAVES waves (round 6: shared by the row's waves, which leaves
 // the hot corner 12-14 KB more), k_scatter2 takes one row's segments in order - so a
@@ -155,13 +156,21 @@ struct Args {
   uint32_t* o_fb;
   uint32_t* o_bfs;
   uint32_t* o_pay;  // big_bfs's payload for traces of 2^21 - 1 spans and more (null when none)
-  // LOG mode: wave gw's log segment starts at lg + lg_start[gw] (= 2 * its first span) and
-  // holds lg_n[gw] entries (cell << 1 | error); lg_cnt[gw * lg_P + p] = its entries in
-  // partition p (cell >> PSHIFT); lg_P partitions, lg_W = k_link's waves
+  // LOG / SORT modes: wave gw's log segment starts at lg + lg_start[gw] (= 2 * its first span)
+  // and holds lg_n[gw] entries (cell << 1 | error); lg_P partitions (cell >> PSHIFT), lg_W =
+  // k_link's waves. LOG mode's block pool (round 6, zdl_log.inc): every k_link workgroup
+  // reserves, per partition p it logged into, ceil(c_p / LBLK) consecutive blocks of lg_pool
+  // (lg_set[PMAX]: the pool cursor) and as many places in p's directory (lg_dir[p * lg_bcap +
+  // r], lg_set[p]: p's blocks so far), and moves its waves' entries there itself; lg_bn[b] =
+  // block b's entries, lg_set[PMAX + 1] = the put's entries
   uint32_t* lg;
   uint64_t* lg_start;
   uint32_t* lg_n;
-  uint32_t* lg_cnt;
+  uint32_t* lg_pool;
+  uint32_t* lg_dir;
+  uint32_t* lg_bn;
+  uint32_t* lg_set;
+  uint32_t lg_bcap;
   uint32_t lg_P, lg_W;
   // ZDL_FLAG_TREE_EXPORT (insertion-order contexts): per span of the put, its node's head
   // slot, its parent's head slot (-1 synthetic root, -2 root, -3 no node) and BFS index
@@ -1653,7 +1662,8 @@ struct zdl_ctx {
   uint32_t epoch = 0;
   DevBuf<uint64_t> cx_win;
   // LOG mode (zdl_log.inc): the emit log, its grouped copy, per-wave segments and counts
-  DevBuf<uint32_t> lg, lg_grp, lg_n, lg_cnt, lg_tot;
+  DevBuf<uint32_t> lg, lg_pool, lg_n, lg_dir, lg_bn, lg_sets;
+  uint32_t lg_par = 0;  // the LOG put's counter set (lg_sets: two of PMAX + 2 words, alternating)
   DevBuf<uint64_t> lg_start;
   int force_tm = -1;  // ZDL_TM=hash|dense|log (tests / ablation): k_link's table mode when it fits
   DevBuf<int32_t> tr_node, tr_parent, tr_bfs;  // ZDL_FLAG_TREE_EXPORT: the last put's tree
@@ -1780,6 +1790,7 @@ struct zdl_ctx {
   uint32_t lk_stride = 1, lk_puts = 0;  // time every lk_stride-th put
   zdl_kernel_times times = {};
   uint32_t last_log_lP = 0;    // the last put's LOG partitions (0: not LOG mode), for log_entries
+  uint32_t* last_log_set = nullptr;  // ... and its counter set
   uint64_t last_sparse_E = 0;  // the last put's sparse link-log entries
   // a lazy put (Args::lazy): launched k_link only; k_mid / k_tail follow only if its flag says
   // so (resolve_lazy), with the put's arguments kept here
@@ -1866,9 +1877,9 @@ void put_times(zdl_ctx* c) {
   c->times.sparse_ms = ev_ms(c, 4, 9);
   c->times.sparse_entries = c->last_sparse_E;
   c->times.log_entries = 0;
-  if (c->last_log_lP) {  // k_pbase's total (the put's work is complete here)
+  if (c->last_log_lP && c->last_log_set) {  // the put's entry count (its work is complete here)
     uint32_t v = 0;
-    if (hipMemcpyAsync(&v, c->lg_tot.p + PMAX + c->last_log_lP, 4, hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
+    if (hipMemcpyAsync(&v, c->last_log_set + PMAX + 1, 4, hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
         hipStreamSynchronize(c->stream) == hipSuccess)
       c->times.log_entries = v;
     (void)hipGetLastError();
@@ -2121,7 +2132,7 @@ void zdl_destroy(zdl_ctx* c) {
     }
   }
   c->prof.release();
-  c->lg.release(); c->lg_grp.release(); c->lg_n.release(); c->lg_cnt.release(); c->lg_tot.release();
+  c->lg.release(); c->lg_pool.release(); c->lg_n.release(); c->lg_dir.release(); c->lg_bn.release(); c->lg_sets.release();
   c->lg_start.release();
   c->tr_node.release(); c->tr_parent.release(); c->tr_bfs.release();
   c->tr_anc.release(); c->tr_link.release(); c->tr_sorted.release(); c->tr_reason.release();
@@ -2657,16 +2668,27 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
     A.tseg_win = c->tseg_win.p;
   }
   if (tm == TM_LOG) {
+    // the pool: every entry (at most 2 a span) plus one partial block per workgroup and partition
+    const uint64_t bcap = (2 * n_spans + LBLK - 1) / LBLK + (uint64_t)lgrid * lP + 1;
+    if (bcap * LBLK >= (1ull << 40) || bcap >= (1ull << 32)) return fail(c, ZDL_EINVAL, "LOG mode: put too large");
     HIP_TRY(c, c->lg.ensure(2 * n_spans));
-    HIP_TRY(c, c->lg_grp.ensure(2 * n_spans));
+    HIP_TRY(c, c->lg_pool.ensure(bcap * LBLK));
+    HIP_TRY(c, c->lg_dir.ensure((size_t)lP * bcap));
+    HIP_TRY(c, c->lg_bn.ensure(bcap));
     HIP_TRY(c, c->lg_start.ensure(lW));
     HIP_TRY(c, c->lg_n.ensure(lW));
-    HIP_TRY(c, c->lg_cnt.ensure((size_t)lP * lW));
-    HIP_TRY(c, c->lg_tot.ensure(2 * PMAX + 1));  // totals, then the bases
+    if (!c->lg_sets.p) {  // both counter sets start at zero; each put's k_hist3 clears the next one's
+      HIP_TRY(c, c->lg_sets.ensure(2 * (PMAX + 2)));
+      HIP_TRY(c, hipMemsetAsync(c->lg_sets.p, 0, 2 * (PMAX + 2) * 4, c->stream));
+    }
     A.lg = c->lg.p;
     A.lg_start = c->lg_start.p;
     A.lg_n = c->lg_n.p;
-    A.lg_cnt = c->lg_cnt.p;
+    A.lg_pool = c->lg_pool.p;
+    A.lg_dir = c->lg_dir.p;
+    A.lg_bn = c->lg_bn.p;
+    A.lg_set = c->lg_sets.p + (size_t)c->lg_par * (PMAX + 2);
+    A.lg_bcap = (uint32_t)bcap;
     A.lg_P = lP;
     A.lg_W = lW;
   }
@@ -2794,14 +2816,13 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   c->last_log_lP = tm == TM_LOG ? lP : 0u;
   c->last_sparse_E = 0;
   if (tm == TM_LOG) {  // group the log by partition, count each partition in LDS (zdl_log.inc)
-    // rows of ZDL_LOG_ROW_WAVES k_link waves, a scatter workgroup per row
-    const uint32_t rows = lW / ZDL_LOG_ROW_WAVES;
-    hipLaunchKernelGGL(k_pscan, dim3(lP), dim3(PSCAN_WG), 0, c->stream, c->lg_cnt.p, rows, lP, c->lg_tot.p);
-    hipLaunchKernelGGL(k_pbase, dim3(1), dim3(PMAX), 0, c->stream, c->lg_tot.p, lP, c->lg_tot.p + PMAX);
-    hipLaunchKernelGGL(k_scatter2, dim3(rows), dim3(SCATTER2_WG), 0, c->stream, c->lg.p, c->lg_start.p,
-                       c->lg_n.p, c->lg_cnt.p, (uint32_t)ZDL_LOG_ROW_WAVES, lP, c->lg_tot.p + PMAX, c->lg_grp.p);
-    hipLaunchKernelGGL(k_hist2, dim3((unsigned)c->cus), dim3(HIST2_WG), 0, c->stream, c->lg_grp.p,
-                       c->lg_tot.p + PMAX, lP, (uint64_t)SS, c->call.p, c->errc.p);
+    // k_link's workgroups moved their entries into the block pool: one kernel counts them
+    uint32_t* const set = A.lg_set;
+    uint32_t* const next = c->lg_sets.p + (size_t)(c->lg_par ^ 1u) * (PMAX + 2);
+    c->last_log_set = set;
+    c->lg_par ^= 1u;
+    hipLaunchKernelGGL(k_hist3, dim3((unsigned)c->cus), dim3(HIST2_WG), 0, c->stream, c->lg_pool.p, c->lg_dir.p,
+                       c->lg_bn.p, (const uint32_t*)set, next, lP, A.lg_bcap, (uint64_t)SS, c->call.p, c->errc.p);
     const hipError_t ke = hipGetLastError();
     if (ke != hipSuccess) {
       c->poisoned = true;
@@ -3447,6 +3468,7 @@ int zdl_reset(zdl_ctx* c) {
   }
   if (c->poisoned) {  // the counter slots may hold a half-finished put's counts
     HIP_TRY(c, hipMemsetAsync(c->counters.p, 0, (CTR_DONE + 1) * 4, c->stream));
+    if (c->lg_sets.p) HIP_TRY(c, hipMemsetAsync(c->lg_sets.p, 0, 2 * (PMAX + 2) * 4, c->stream));
     c->poisoned = false;
   }
   const size_t SS = c->sparse ? 0 : (size_t)c->rows * c->S;  // sparse: only the status word
