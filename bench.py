@@ -1000,12 +1000,12 @@ def main():
         rms = float(kt.reduce_ms)
         gbs = 4 * ent / (rms * 1e-3) / 1e9 if rms > 0 else None
         log_reduce = {"ms": rms, "entries": ent, "algorithmic_bytes": 4 * ent,
-                      "moved_bytes_model": 12 * ent,
+                      "moved_bytes_model": 4 * ent,
                       "achieved_gbs": gbs, "frac": gbs / HBM_PEAK_GBS if gbs else None,
                       "k_link_ms_same_put": float(kt.tiles_ms),
-                      "note": "k_pscan + k_pbase + k_scatter2 + k_hist2 of one put (HIP events); algorithmic: "
-                              "the log read once (4 B/entry); the kernels move 12 B/entry (scatter reads "
-                              "and writes it, hist reads it) plus the per-row partition counts"}
+                      "note": "k_hist3 of one put (HIP events): the block pool read once (4 B/entry); k_link's "
+                              "workgroups moved the log into the pool by partition at their ends (8 B/entry, "
+                              "inside k_link's time)"}
     ctxs = []
     if dist:
         tt = torch.tensor([elapsed], dtype=torch.float64)
