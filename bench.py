@@ -804,7 +804,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=20,
+                    help="untimed steps before the timed ones (the first steps of a run are slower than the later ones)")
     ap.add_argument("--config", default=None, help="default: c2 at N = 1, c3 (per-GPU shard) at N > 1")
     ap.add_argument("--traces", type=int, default=0, help="override traces per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
