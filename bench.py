@@ -804,8 +804,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=20,
-                    help="untimed steps before the timed ones (the first steps of a run are slower than the later ones)")
+    ap.add_argument("--warmup", type=int, default=20, help="untimed steps before the timed ones")
+    ap.add_argument("--warm-ms", type=float, default=200.0,
+                    help="after the --warmup steps, more untimed steps until the warm-up has lasted this long "
+                         "(the GPU's clocks ramp over the first ~50 ms of load: profiles/r06i_warm_probe.txt)")
     ap.add_argument("--config", default=None, help="default: c2 at N = 1, c3 (per-GPU shard) at N > 1")
     ap.add_argument("--traces", type=int, default=0, help="override traces per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -936,7 +938,23 @@ def main():
             c.sync()
         torch.cuda.synchronize(dev)
 
+    # Warm-up: --warmup steps, then more in chunks until --warm-ms have passed (every rank runs the
+    # same number: with RCCL each link() is a collective). A run's first ~50 ms of steps are up to
+    # 20 % slower than the steady state whatever the step count (profiles/r06i_warm_probe.txt).
+    t_warm = time.perf_counter()
     run(args.warmup)
+    warm_steps = args.warmup
+    chunk = max(inflight * 4, 8)
+    while True:
+        sync_all()
+        more = torch.tensor([1 if (time.perf_counter() - t_warm) * 1e3 < args.warm_ms else 0])
+        if dist:
+            dist.all_reduce(more, op=dist.ReduceOp.MAX)
+        if not int(more):
+            break
+        run(chunk)
+        warm_steps += chunk
+    warm_ms = (time.perf_counter() - t_warm) * 1e3
     for c in ctxs:
         c.kernel_times()  # drops the warmup puts from the k_link event rings
     if dist:
@@ -1204,7 +1222,8 @@ def main():
             "data": "synthetic",
             "config": {"workload": w.name, "spans_per_gpu": cols.n_spans, "traces_per_gpu": cols.n_traces,
                        "services": S, "parallelism": f"trace-shard x{world}", "combine": combine,
-                       "inflight": inflight, "ms_per_step_serial": serial_ms,
+                       "inflight": inflight, "warm_up": {"steps": warm_steps, "ms": warm_ms},
+                       "ms_per_step_serial": serial_ms,
                        "ms_per_step_shared_input": shared_ms,
                        "interleaved_legs": legs,
                        "step_roofline_frac_serial": (bytes_launch / (serial_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
