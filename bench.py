@@ -377,7 +377,7 @@ def _small_bytes(sizes, n_traces):
     return BYTES_PER_SPAN * int(sizes[sizes <= 64].sum()) + BYTES_PER_TRACE * (n_traces + 1)
 
 
-def c5_leg(device, steps=16, parity=True, threads=16, host_threads=2):
+def c5_leg(device, steps=16, parity=True, threads=16, host_threads=2, warm_ms=200.0):
     """BASELINE.json configs[4] (C5: 10 000 services, Zipf(1.1), depth 64, fan-out <= 1000,
     Pareto(1.2) trace sizes clipped to [1, 200 000]: 81.1M spans / 16M traces) on one GPU, a
     sparse context (the link list sorted by cell, no S x S table). One step = reset, put of the
@@ -422,26 +422,34 @@ def c5_leg(device, steps=16, parity=True, threads=16, host_threads=2):
     outs = [None, None]
     errs = []
 
-    def worker(j):
+    def worker(j, n):
         try:
-            for _ in range(j, steps, 2):
+            for _ in range(j, n, 2):
                 put(ctxs[j])
                 outs[j] = ctxs[j].link_finish(copy=False)
         except Exception as e:  # surfaced after the join
             errs.append(e)
-    th = [threading.Thread(target=worker, args=(j,)) for j in range(2)]
+
+    def run(n):
+        if host_threads == 2:
+            th = [threading.Thread(target=worker, args=(j, n)) for j in range(2)]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+        else:  # one host thread alternating the contexts (A/B)
+            for k in range(n):
+                put(ctxs[k % 2])
+                if k:
+                    outs[(k - 1) % 2] = ctxs[(k - 1) % 2].link_finish(copy=False)
+            outs[(n - 1) % 2] = ctxs[(n - 1) % 2].link_finish(copy=False)
+        if errs:
+            raise errs[0]
+    t_w = time.perf_counter()
+    while (time.perf_counter() - t_w) * 1e3 < warm_ms:  # warm-up: the generation left the GPU idle
+        run(8)
     t1 = time.perf_counter()
-    if host_threads == 2:
-        for t in th:
-            t.start()
-        for t in th:
-            t.join()
-    else:  # one host thread alternating the contexts (A/B)
-        for k in range(steps):
-            put(ctxs[k % 2])
-            if k:
-                outs[(k - 1) % 2] = ctxs[(k - 1) % 2].link_finish(copy=False)
-        outs[(steps - 1) % 2] = ctxs[(steps - 1) % 2].link_finish(copy=False)
+    run(steps)
     ms = (time.perf_counter() - t1) / steps * 1e3
     if errs:
         raise errs[0]
@@ -611,7 +619,7 @@ def cpu_info():
     return {"nproc": nproc, "affinity": aff, "quota": quota, "usable": usable, "model": model, "why": why}
 
 
-def c3_job_leg(device, ranks=8, traces_per_rank=C3_TRACES_PER_GPU, steps=5, parity=True, threads=16):
+def c3_job_leg(device, ranks=8, traces_per_rank=C3_TRACES_PER_GPU, steps=5, parity=True, threads=16, warm_ms=200.0):
     """BASELINE.json configs[2] as stated - 1B synthetic spans / 100M traces / 500 services sharded
     by splitmix64(trace_lo) over 8 ranks, the ranks' counts combined (DependencyLinker.merge's sum,
     DependencyLinker.java:189-204) - on ONE MI355X: the 8 ranks are contexts of this process joined
@@ -713,7 +721,11 @@ def c3_job_leg(device, ranks=8, traces_per_rank=C3_TRACES_PER_GPU, steps=5, pari
         links = max(m[2] for m in marks) - max(m[1] for m in marks)
         return (t2 - t1) * 1e3, puts * 1e3, links * 1e3
 
-    step(False)  # warmup
+    t_w = time.perf_counter()
+    while True:  # warm-up: at least one step and warm_ms of load (the generation left the GPU idle)
+        step(False)
+        if (time.perf_counter() - t_w) * 1e3 >= warm_ms:
+            break
     job = [step(False)[0] for _ in range(steps)]
     ph = [step(True) for _ in range(steps)]
     ranks_agree = all(all(np.array_equal(a, b) for a, b in zip(out[0], out[r])) for r in range(ranks))
@@ -1084,7 +1096,11 @@ def main():
                 res = ictxs[k % inflight_i].link(N.ZDL_ORDER_INSERTION)
             return res
 
-        irun(3, 2)
+        t_w = time.perf_counter()
+        while True:  # warm-up (the contexts' setup left the GPU idle for a few ms)
+            irun(8, 2)
+            if (time.perf_counter() - t_w) * 1e3 >= args.warm_ms / 2:
+                break
         for ic in ictxs:
             ic.sync()
         ik = max(args.steps, 10)
@@ -1152,13 +1168,14 @@ def main():
             f"({fpt['us_per_call']:.1f} us/call, {fpt['spans_per_s']:.3e} spans/s), links {fpt['parity']}")
     c5 = None
     if side and not args.no_c5:
-        c5 = c5_leg(local, parity=not args.no_parity, threads=cpu_info()["usable"], host_threads=args.c5_host_threads)
+        c5 = c5_leg(local, parity=not args.no_parity, threads=cpu_info()["usable"], host_threads=args.c5_host_threads,
+                    warm_ms=args.warm_ms)
         log(f"c5: {c5['ms_per_step']:.2f} ms/step ({c5['spans_per_s']:.3e} spans/s), links {c5['parity']}, "
             + ", ".join(f"{k} {v['ms']:.3f} ms" for k, v in c5["phases"].items() if v["ms"] is not None))
     c3job = None
     if side and not args.no_c3_job:
         c3job = c3_job_leg(local, traces_per_rank=args.c3_job_traces, parity=not args.no_parity,
-                           threads=cpu_info()["usable"])
+                           threads=cpu_info()["usable"], warm_ms=args.warm_ms)
         log(f"c3 job (1B spans, 8 ranks on one GPU): {c3job['ms_per_job_step']:.2f} ms/job step "
             f"({c3job['spans_per_s']:.3e} spans/s), puts {c3job['phased']['puts_ms']:.2f} ms, link phase "
             f"{c3job['phased']['link_phase_ms']:.2f} ms (combine {c3job['phased']['combine_ms']:.2f} ms), "
