@@ -1512,12 +1512,19 @@ __global__ void k_merge_compact(const unsigned long long* __restrict__ tcall, co
 // Insertion order, tables of at most MAP_CAP cells: the non-empty cells (first rank set) with
 // their counts and first ranks written straight into mapped pinned host memory (meta[0] the
 // status, meta[1] the count, then parent, child, call, err, first columns of MAP_CAP each) by
-// one workgroup, so link() costs one kernel and one wait; the host orders the records by rank.
+// one workgroup IN RANK ORDER (DependencyLinker.link()'s list order), so link() costs one kernel,
+// one wait and no host work: the cells are compacted into LDS (rank, cell) pairs and
+// bitonic-sorted there (ranks are distinct: one addLink, one cell). Round 6 sorted the records
+// on the host (std::sort, ~20-30 us of the step's host time at C2's 2 500 links).
+constexpr size_t ORD_COMPACT_LDS = (size_t)MAP_CAP * 12;  // u64 ranks, then u32 cells
 __global__ void __launch_bounds__(COMPACT_WG) k_ord_compact(const unsigned long long* __restrict__ tcall,
                                                             const unsigned long long* __restrict__ terr,
                                                             const unsigned long long* __restrict__ tfirst, uint32_t SS,
                                                             uint32_t S, const uint32_t* __restrict__ status,
                                                             unsigned long long* __restrict__ meta) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  unsigned long long* const sk = reinterpret_cast<unsigned long long*>(lds);
+  uint32_t* const sv = reinterpret_cast<uint32_t*>(lds + 8 * MAP_CAP);
   __shared__ uint32_t wsum[COMPACT_WG / 64 + 1];
   constexpr int KMAX = 8;
   const uint32_t K = (SS + COMPACT_WG - 1) / COMPACT_WG, c0 = threadIdx.x * K;
@@ -1544,27 +1551,55 @@ __global__ void __launch_bounds__(COMPACT_WG) k_ord_compact(const unsigned long 
       wsum[i] = acc;
       acc += t;
     }
+    wsum[COMPACT_WG / 64] = acc;
     meta[0] = *status;
     meta[1] = acc;
   }
   __syncthreads();
+  uint32_t o = wsum[w] + incl - nz;
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) {
+    if (fv[k] == ~0ull) continue;
+    sk[o] = fv[k];
+    sv[o] = c0 + k;
+    ++o;
+  }
+  const uint32_t m = wsum[COMPACT_WG / 64];
+  uint32_t np = 1;
+  while (np < m) np <<= 1;
+  for (uint32_t i = m + threadIdx.x; i < np; i += COMPACT_WG) {  // sentinels after the records
+    sk[i] = ~0ull;
+    sv[i] = ~0u;
+  }
+  __syncthreads();
+  for (uint32_t k = 2; k <= np; k <<= 1)  // ascending bitonic sort of (rank, cell) by rank
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      for (uint32_t t = threadIdx.x; t < np / 2; t += COMPACT_WG) {
+        const uint32_t i = 2 * t - (t & (j - 1)), l = i + j;
+        const unsigned long long a = sk[i], b = sk[l];
+        if ((a > b) == ((i & k) == 0)) {
+          sk[i] = b;
+          sk[l] = a;
+          const uint32_t x = sv[i];
+          sv[i] = sv[l];
+          sv[l] = x;
+        }
+      }
+      __syncthreads();
+    }
   unsigned char* b = reinterpret_cast<unsigned char*>(meta) + 16;
   int32_t* op = reinterpret_cast<int32_t*>(b);
   int32_t* oc = reinterpret_cast<int32_t*>(b + 4 * MAP_CAP);
   int64_t* ocall = reinterpret_cast<int64_t*>(b + 8 * MAP_CAP);
   int64_t* oerr = reinterpret_cast<int64_t*>(b + 16 * MAP_CAP);
   uint64_t* ofirst = reinterpret_cast<uint64_t*>(b + 24 * MAP_CAP);
-  uint32_t o = wsum[w] + incl - nz;
-#pragma unroll
-  for (int k = 0; k < KMAX; ++k) {
-    if (fv[k] == ~0ull) continue;
-    const uint32_t i = c0 + k;
-    op[o] = (int32_t)(i / S);
-    oc[o] = (int32_t)(i % S);
-    ocall[o] = (int64_t)tcall[i];
-    oerr[o] = (int64_t)terr[i];
-    ofirst[o] = fv[k];
-    ++o;
+  for (uint32_t i = threadIdx.x; i < m; i += COMPACT_WG) {  // consecutive records a wave: coalesced
+    const uint32_t cell = sv[i];
+    op[i] = (int32_t)(cell / S);
+    oc[i] = (int32_t)(cell % S);
+    ocall[i] = (int64_t)tcall[cell];
+    oerr[i] = (int64_t)terr[cell];
+    ofirst[i] = sk[i];
   }
 }
 
@@ -1648,7 +1683,7 @@ struct zdl_ctx {
   DevBuf<unsigned long long> first, o_key;
   DevBuf<uint64_t> ord_n;  // insertion order, mode 6: the traces zdl_ord.inc's pass ranks
   DevBuf<unsigned long long> ord_w;  // ... and the first simple trace of each pair (Args::ord_w),
-  DevBuf<unsigned long long> ord_log, ord_part;  // the waves' records, k_ord_reduce's partials
+  DevBuf<unsigned long long> ord_log;  // the waves' records
   DevBuf<uint64_t> ord_start;
   DevBuf<uint32_t> ord_cnt;
 
@@ -2028,6 +2063,8 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
     if (e == hipSuccess)
       e = hipFuncSetAttribute(k_ord_rank_fn(w), hipFuncAttributeMaxDynamicSharedMemorySize, (int)tail_block_bytes(w));
   }
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)k_ord_compact, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ORD_COMPACT_LDS);
   if (e == hipSuccess) {
     const char* pe = getenv("ZDL_PROF");
     c->prof_on = pe && pe[0] == '1';
@@ -2088,7 +2125,7 @@ void zdl_destroy(zdl_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (auto& r : c->rank) r.release();
   c->call.release(); c->errc.release(); c->status.release();
-  c->first.release(); c->ord_n.release(); c->ord_w.release(); c->ord_log.release(); c->ord_part.release();
+  c->first.release(); c->ord_n.release(); c->ord_w.release(); c->ord_log.release();
   c->ord_start.release(); c->ord_cnt.release(); c->day_first.release(); c->o_key.release(); c->o_fa.release(); c->o_fb.release(); c->o_bfs.release(); c->o_pay.release();
   c->big_list.release(); c->big_stat.release(); c->big_exact_list.release(); c->counters.release(); c->retry.release();
   c->cx_win.release();
@@ -2757,7 +2794,9 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   }
   if (c->ord) {
     HIP_TRY(c, c->ord_n.ensure(1));
+    const bool fresh_w = c->ord_w.n < SS;
     HIP_TRY(c, c->ord_w.ensure(SS));
+    if (fresh_w) HIP_TRY(c, hipMemsetAsync(c->ord_w.p, 0xFF, SS * 8, c->stream));  // (k_ord_reduce's atomicMin)
     if (lmode == 6) {
       if ((lW + ORD_RED_G - 1) / ORD_RED_G > (uint32_t)ORD_RED_MAXW)
         return fail(c, ZDL_EINVAL, "insertion order: too many k_link waves for k_ord_reduce");
@@ -2768,7 +2807,6 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
       HIP_TRY(c, c->ord_log.ensure(std::max<uint64_t>(1, std::min<uint64_t>(2 * n_spans, full))));
       HIP_TRY(c, c->ord_start.ensure(lW));
       HIP_TRY(c, c->ord_cnt.ensure(lW));
-      HIP_TRY(c, c->ord_part.ensure((size_t)ORD_RED_G * SS));
       A.ord_log = c->ord_log.p;
       A.ord_start = c->ord_start.p;
       A.ord_cnt = c->ord_cnt.p;
@@ -2883,9 +2921,7 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   if (A.map) c->seq = A.seq;
   if (lmode == 6) {  // the pairs' first simple traces ranked exactly (zdl_ord.inc); cx_win is free again
     hipLaunchKernelGGL(k_ord_reduce, dim3(ORD_RED_G), dim3(ORD_RED_WG), (size_t)SS * 8, c->stream, c->ord_log.p,
-                       c->ord_start.p, c->ord_cnt.p, lW, (uint32_t)SS, c->ord_part.p);
-    hipLaunchKernelGGL(k_ord_final, dim3((unsigned)((SS + 255) / 256)), dim3(256), 0, c->stream, c->ord_part.p,
-                       (uint32_t)SS, c->ord_w.p);
+                       c->ord_start.p, c->ord_cnt.p, lW, (uint32_t)SS, c->ord_w.p);
     hipLaunchKernelGGL(k_ord_winners, dim3(1), dim3(OW_WG), 0, c->stream, c->ord_w.p, (uint32_t)SS, n_spans,
                        c->cx_win.p, c->ord_n.p, c->status.p);
     Args R = A;
@@ -3469,6 +3505,7 @@ int zdl_reset(zdl_ctx* c) {
   if (c->poisoned) {  // the counter slots may hold a half-finished put's counts
     HIP_TRY(c, hipMemsetAsync(c->counters.p, 0, (CTR_DONE + 1) * 4, c->stream));
     if (c->lg_sets.p) HIP_TRY(c, hipMemsetAsync(c->lg_sets.p, 0, 2 * (PMAX + 2) * 4, c->stream));
+    if (c->ord_w.p) HIP_TRY(c, hipMemsetAsync(c->ord_w.p, 0xFF, c->ord_w.n * 8, c->stream));  // all ones between puts
     c->poisoned = false;
   }
   const size_t SS = c->sparse ? 0 : (size_t)c->rows * c->S;  // sparse: only the status word
@@ -3516,8 +3553,8 @@ static int link_insertion(zdl_ctx* c, zdl_links* out, const unsigned long long* 
       HIP_TRY(c, hipHostMalloc((void**)&c->h_ordmap, 16 + 32 * MAP_CAP, hipHostMallocMapped | hipHostMallocCoherent));
       HIP_TRY(c, hipHostGetDevicePointer((void**)&c->d_ordmap, c->h_ordmap, 0));
     }
-    hipLaunchKernelGGL(k_ord_compact, dim3(1), dim3(COMPACT_WG), 0, c->stream, call, errc, first_rank, (uint32_t)SS,
-                       c->S, c->status.p, c->d_ordmap);
+    hipLaunchKernelGGL(k_ord_compact, dim3(1), dim3(COMPACT_WG), ORD_COMPACT_LDS, c->stream, call, errc, first_rank,
+                       (uint32_t)SS, c->S, c->status.p, c->d_ordmap);
     HIP_TRY(c, hipGetLastError());
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     put_times(c);
@@ -3529,21 +3566,10 @@ static int link_insertion(zdl_ctx* c, zdl_links* out, const unsigned long long* 
     const int32_t* ch = reinterpret_cast<const int32_t*>(b + 4 * MAP_CAP);
     const int64_t* ca = reinterpret_cast<const int64_t*>(b + 8 * MAP_CAP);
     const int64_t* er = reinterpret_cast<const int64_t*>(b + 16 * MAP_CAP);
-    const uint64_t* fr = reinterpret_cast<const uint64_t*>(b + 24 * MAP_CAP);
-    std::vector<std::pair<uint64_t, uint32_t>> key(m);
-    for (size_t i = 0; i < m; ++i) key[i] = {fr[i], (uint32_t)i};
-    std::sort(key.begin(), key.end());
-    c->out_p.resize(m);
-    c->out_c.resize(m);
-    c->out_call.resize(m);
-    c->out_err.resize(m);
-    for (size_t i = 0; i < m; ++i) {
-      const uint32_t j = key[i].second;
-      c->out_p[i] = p[j];
-      c->out_c[i] = ch[j];
-      c->out_call[i] = ca[j];
-      c->out_err[i] = er[j];
-    }
+    c->out_p.assign(p, p + m);  // already in rank order (k_ord_compact)
+    c->out_c.assign(ch, ch + m);
+    c->out_call.assign(ca, ca + m);
+    c->out_err.assign(er, er + m);
     out->n = m;
     out->parent = c->out_p.data();
     out->child = c->out_c.data();
