@@ -1511,95 +1511,103 @@ __global__ void k_merge_compact(const unsigned long long* __restrict__ tcall, co
 
 // Insertion order, tables of at most MAP_CAP cells: the non-empty cells (first rank set) with
 // their counts and first ranks written straight into mapped pinned host memory (meta[0] the
-// status, meta[1] the count, then parent, child, call, err, first columns of MAP_CAP each) by
-// one workgroup IN RANK ORDER (DependencyLinker.link()'s list order), so link() costs one kernel,
-// one wait and no host work: the cells are compacted into LDS (rank, cell) pairs and
-// bitonic-sorted there (ranks are distinct: one addLink, one cell). Round 6 sorted the records
-// on the host (std::sort, ~20-30 us of the step's host time at C2's 2 500 links).
-constexpr size_t ORD_COMPACT_LDS = (size_t)MAP_CAP * 12;  // u64 ranks, then u32 cells
-__global__ void __launch_bounds__(COMPACT_WG) k_ord_compact(const unsigned long long* __restrict__ tcall,
-                                                            const unsigned long long* __restrict__ terr,
-                                                            const unsigned long long* __restrict__ tfirst, uint32_t SS,
-                                                            uint32_t S, const uint32_t* __restrict__ status,
-                                                            unsigned long long* __restrict__ meta) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  unsigned long long* const sk = reinterpret_cast<unsigned long long*>(lds);
-  uint32_t* const sv = reinterpret_cast<uint32_t*>(lds + 8 * MAP_CAP);
-  __shared__ uint32_t wsum[COMPACT_WG / 64 + 1];
-  constexpr int KMAX = 8;
-  const uint32_t K = (SS + COMPACT_WG - 1) / COMPACT_WG, c0 = threadIdx.x * K;
-  unsigned long long fv[KMAX];
-  uint32_t nz = 0;
-#pragma unroll
-  for (int k = 0; k < KMAX; ++k) {
-    fv[k] = (uint32_t)k < K && c0 + k < SS ? tfirst[c0 + k] : ~0ull;
-    nz += fv[k] != ~0ull ? 1u : 0u;
-  }
+// status, meta[1] the count, then parent, child, call, err, first columns of MAP_CAP each) IN
+// RANK ORDER (DependencyLinker.link()'s list order), so link() costs one kernel, one wait and no
+// host sort. Wave w of the grid takes cells w + k NW (k < OC_KEYS): a non-empty cell's place is
+// the number of smaller first ranks in the table (ranks are distinct: one addLink, one cell;
+// empty cells hold all ones). The wave sweeps the L2-resident table once, OC_BATCH x 64 cells a
+// batch (their loads in flight together), comparing each batch against all its cells' ranks
+// (a ballot and a popcount per 64), then stores each (rank, cell) at its place. No LDS and
+// 256-thread workgroups, so the kernel fits beside the other in-flight context's k_link. The
+// workgroup whose ticket comes last (MI355X_MICROARCH.md "Valid forms": every storing wave waits
+// vmcnt(0), a barrier, an agent release, the ticket; the last one acquires) writes the columns.
+// Round 6 first sorted on the host (std::sort, ~20-30 us of the step's host time at C2's 2 500
+// links), then in one workgroup's LDS (a bitonic sort: 50-150 us), then in 96 KB of LDS per
+// workgroup (which waited for the other context's k_link to leave a CU: 79 us in flight), then
+// a sweep of the table per record (latency-bound: 195 us).
+constexpr int OC_WG = 256, ORD_SORT_G = 256, OC_KEYS = 8, OC_BATCH = 16;
+static_assert((size_t)ORD_SORT_G * (OC_WG / 64) * OC_KEYS >= MAP_CAP, "k_ord_compact covers every cell");
+__global__ void __launch_bounds__(OC_WG) k_ord_compact(const unsigned long long* __restrict__ tcall,
+                                                       const unsigned long long* __restrict__ terr,
+                                                       const unsigned long long* __restrict__ tfirst, uint32_t SS,
+                                                       uint32_t S, const uint32_t* __restrict__ status,
+                                                       unsigned long long* __restrict__ meta,
+                                                       unsigned long long* __restrict__ srank,
+                                                       uint32_t* __restrict__ scell, uint32_t* __restrict__ done) {
+  __shared__ uint32_t last, wcnt[OC_WG / 64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  uint32_t incl = nz;
+  const uint32_t nw = gridDim.x * (OC_WG / 64), gw = blockIdx.x * (OC_WG / 64) + (uint32_t)w;
+  unsigned long long key[OC_KEYS];
+  uint32_t below[OC_KEYS];
 #pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(incl, d, 64);
-    if (lane >= d) incl += y;
+  for (int k = 0; k < OC_KEYS; ++k) {
+    const uint32_t c = gw + (uint32_t)k * nw;
+    key[k] = c < SS ? tfirst[c] : ~0ull;
+    below[k] = 0;
   }
-  if (lane == 63) wsum[w] = incl;
+  for (uint32_t j0 = 0; j0 < SS; j0 += 64 * OC_BATCH) {
+    unsigned long long v[OC_BATCH];
+#pragma unroll
+    for (int q = 0; q < OC_BATCH; ++q) {
+      const uint32_t j = j0 + (uint32_t)(q * 64 + lane);
+      v[q] = j < SS ? tfirst[j] : ~0ull;
+    }
+#pragma unroll
+    for (int k = 0; k < OC_KEYS; ++k) {
+      if (key[k] == ~0ull) continue;  // (uniform)
+      uint32_t n = 0;
+#pragma unroll
+      for (int q = 0; q < OC_BATCH; ++q) n += (uint32_t)__popcll(__ballot(v[q] < key[k]));
+      below[k] += n;
+    }
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < OC_KEYS; ++k) {
+      if (key[k] == ~0ull) continue;
+      srank[below[k]] = key[k];
+      scell[below[k]] = gw + (uint32_t)k * nw;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    uint32_t acc = 0;
-    for (int i = 0; i < COMPACT_WG / 64; ++i) {
-      const uint32_t t = wsum[i];
-      wsum[i] = acc;
-      acc += t;
-    }
-    wsum[COMPACT_WG / 64] = acc;
-    meta[0] = *status;
-    meta[1] = acc;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   }
   __syncthreads();
-  uint32_t o = wsum[w] + incl - nz;
+  if (!last) return;
+  if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  uint32_t n = 0;  // the record count: the non-empty cells
+  for (uint32_t c = threadIdx.x; c < SS; c += OC_WG) n += tfirst[c] != ~0ull ? 1u : 0u;
 #pragma unroll
-  for (int k = 0; k < KMAX; ++k) {
-    if (fv[k] == ~0ull) continue;
-    sk[o] = fv[k];
-    sv[o] = c0 + k;
-    ++o;
-  }
-  const uint32_t m = wsum[COMPACT_WG / 64];
-  uint32_t np = 1;
-  while (np < m) np <<= 1;
-  for (uint32_t i = m + threadIdx.x; i < np; i += COMPACT_WG) {  // sentinels after the records
-    sk[i] = ~0ull;
-    sv[i] = ~0u;
-  }
+  for (int d = 32; d > 0; d >>= 1) n += __shfl_xor(n, d, 64);
+  if (lane == 0) wcnt[w] = n;
   __syncthreads();
-  for (uint32_t k = 2; k <= np; k <<= 1)  // ascending bitonic sort of (rank, cell) by rank
-    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-      for (uint32_t t = threadIdx.x; t < np / 2; t += COMPACT_WG) {
-        const uint32_t i = 2 * t - (t & (j - 1)), l = i + j;
-        const unsigned long long a = sk[i], b = sk[l];
-        if ((a > b) == ((i & k) == 0)) {
-          sk[i] = b;
-          sk[l] = a;
-          const uint32_t x = sv[i];
-          sv[i] = sv[l];
-          sv[l] = x;
-        }
-      }
-      __syncthreads();
-    }
+  uint32_t m = 0;
+#pragma unroll
+  for (int k = 0; k < OC_WG / 64; ++k) m += wcnt[k];
+  if (threadIdx.x == 0) {
+    *done = 0;  // for the next launch (stream-ordered)
+    meta[0] = *status;
+    meta[1] = m;
+  }
   unsigned char* b = reinterpret_cast<unsigned char*>(meta) + 16;
   int32_t* op = reinterpret_cast<int32_t*>(b);
   int32_t* oc = reinterpret_cast<int32_t*>(b + 4 * MAP_CAP);
   int64_t* ocall = reinterpret_cast<int64_t*>(b + 8 * MAP_CAP);
   int64_t* oerr = reinterpret_cast<int64_t*>(b + 16 * MAP_CAP);
   uint64_t* ofirst = reinterpret_cast<uint64_t*>(b + 24 * MAP_CAP);
-  for (uint32_t i = threadIdx.x; i < m; i += COMPACT_WG) {  // consecutive records a wave: coalesced
-    const uint32_t cell = sv[i];
+  for (uint32_t i = threadIdx.x; i < m; i += OC_WG) {  // consecutive records a wave: coalesced
+    const uint32_t cell = scell[i];
     op[i] = (int32_t)(cell / S);
     oc[i] = (int32_t)(cell % S);
     ocall[i] = (int64_t)tcall[cell];
     oerr[i] = (int64_t)terr[cell];
-    ofirst[i] = sk[i];
+    ofirst[i] = srank[i];
   }
 }
 
@@ -1786,6 +1794,7 @@ struct zdl_ctx {
   unsigned long long* d_ordmap = nullptr;
   unsigned long long* d_map = nullptr;  // its device address
   bool map_fresh = false;               // h_map holds the compaction of the current table
+  bool ordmap_fresh = false;            // h_ordmap holds the insertion-order compaction of the current table
   bool poisoned = false;                // a put stopped between its kernels: zdl_reset required
   unsigned long long* h_flag = nullptr;  // mapped pinned: the last put's k_tail stores its seq
   unsigned long long* d_flag = nullptr;
@@ -1807,6 +1816,8 @@ struct zdl_ctx {
   bool rec_job = false;  // a record copy is pending (run by rec_wait, or by rec_th once launched)
   size_t rec_off[4] = {}, rec_len[4] = {};
   DevBuf<uint64_t> o_first;
+  DevBuf<unsigned long long> oc_rank;  // k_ord_compact: (rank, cell) by place, and its ticket
+  DevBuf<uint32_t> oc_cell, oc_done;
   DevBuf<int32_t> mi_p, mi_c;
   DevBuf<int64_t> mi_call, mi_err;
   std::vector<int32_t> out_p, out_c;
@@ -1948,6 +1959,8 @@ static void stage_drop(zdl_ctx* c);                // ... discarded (zdl_reset)
 static void stage_free(zdl_ctx* c);
 static int rec_wait(zdl_ctx* c);  // the SDMA record copy of the last link (ZDL_REC_SDMA)
 static int x_failed(zdl_ctx* c, int rc);  // a failed combine breaks a local world (zdl_xport.inc)
+static int ord_compact(zdl_ctx* c, const unsigned long long* call, const unsigned long long* errc,
+                       const unsigned long long* first_rank);  // insertion order into h_ordmap
 
 // splitmix64 finaliser (shard.py's): trace t goes to device splitmix64(trace_lo) % n
 inline uint64_t splitmix64(uint64_t x) {
@@ -2063,8 +2076,7 @@ zdl_ctx* zdl_create(const zdl_config* cfg) {
     if (e == hipSuccess)
       e = hipFuncSetAttribute(k_ord_rank_fn(w), hipFuncAttributeMaxDynamicSharedMemorySize, (int)tail_block_bytes(w));
   }
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)k_ord_compact, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ORD_COMPACT_LDS);
+
   if (e == hipSuccess) {
     const char* pe = getenv("ZDL_PROF");
     c->prof_on = pe && pe[0] == '1';
@@ -2199,6 +2211,7 @@ void zdl_destroy(zdl_ctx* c) {
   c->g_ip6.release(); c->g_pf.release(); c->g_ts.release();
   c->count.release(); c->m_call.release(); c->m_err.release(); c->m_first.release();
   c->o_p.release(); c->o_c.release(); c->o_call.release(); c->o_err.release(); c->o_first.release();
+  c->oc_rank.release(); c->oc_cell.release(); c->oc_done.release();
   c->o_links.release();
   if (c->h_meta) (void)hipHostFree(c->h_meta);
   if (c->h_map) (void)hipHostFree(c->h_map);
@@ -2268,6 +2281,7 @@ int zdl_set_days(zdl_ctx* c, int64_t day0_ms, uint32_t n_days) {
   if (c->ord) HIP_TRY(c, c->first.ensure(SS));
   if (n_days) HIP_TRY(c, c->day_first.ensure(n_days));
   c->map_fresh = false;
+  c->ordmap_fresh = false;
   return zdl_reset(c);
 }
 
@@ -2869,6 +2883,7 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
   }
   ev_record(c, 2);
   c->map_fresh = false;  // k_link has changed the table
+  c->ordmap_fresh = false;
   if (A.lazy) {
     c->lazy_A = A;
     c->lazy_wmode = wmode;
@@ -2946,10 +2961,16 @@ static int put_spans_link(zdl_ctx* c, const zdl_span_cols* col, uint64_t n_spans
       c->span_base += n_spans;
       ++c->epoch;
       c->map_fresh = false;
+  c->ordmap_fresh = false;
       return rc;
     }
   }
   c->span_base += n_spans;  // the next put's traces come after this one's
+  if (c->ord && !c->days && SS <= MAP_CAP && !in_job(c)) {  // zdl_link's compaction, queued behind the put
+    const int orc = ord_compact(c, c->call.p, c->errc.p, c->first.p);
+    if (orc != ZDL_OK) return orc;
+    c->ordmap_fresh = true;
+  }
   ev_record(c, 9);
   ++c->epoch;  // k_tail zeroed the other counter slots
   c->map_fresh = A.map != nullptr;
@@ -3516,6 +3537,7 @@ int zdl_reset(zdl_ctx* c) {
   if (c->days) HIP_TRY(c, hipMemsetAsync(c->day_first.p, 0xff, (size_t)c->days * 8, c->stream));
   HIP_TRY(c, hipGetLastError());
   c->map_fresh = false;
+  c->ordmap_fresh = false;
   return ZDL_OK;  // stream-ordered: no host wait
 }
 
@@ -3545,17 +3567,35 @@ static void sort_output(zdl_ctx* c, size_t n) {
 
 // zdl_link in ZDL_ORDER_INSERTION: the non-zero cells with their first-addLink ranks
 // (k_merge_compact over the context's tables), ordered by rank.
+// k_ord_compact of (call, errc, first_rank) into the mapped buffer h_ordmap (tables of at most
+// MAP_CAP cells), queued on the context's stream
+static int ord_compact(zdl_ctx* c, const unsigned long long* call, const unsigned long long* errc,
+                       const unsigned long long* first_rank) {
+  const uint64_t SS = (uint64_t)c->rows * c->S;
+  if (!c->h_ordmap) {
+    HIP_TRY(c, hipHostMalloc((void**)&c->h_ordmap, 16 + 32 * MAP_CAP, hipHostMallocMapped | hipHostMallocCoherent));
+    HIP_TRY(c, hipHostGetDevicePointer((void**)&c->d_ordmap, c->h_ordmap, 0));
+  }
+  if (!c->oc_done.p) {
+    HIP_TRY(c, c->oc_done.ensure(1));
+    HIP_TRY(c, hipMemsetAsync(c->oc_done.p, 0, 4, c->stream));
+  }
+  HIP_TRY(c, c->oc_rank.ensure(MAP_CAP));
+  HIP_TRY(c, c->oc_cell.ensure(MAP_CAP));
+  hipLaunchKernelGGL(k_ord_compact, dim3(ORD_SORT_G), dim3(OC_WG), 0, c->stream, call, errc, first_rank,
+                     (uint32_t)SS, c->S, c->status.p, c->d_ordmap, c->oc_rank.p, c->oc_cell.p, c->oc_done.p);
+  HIP_TRY(c, hipGetLastError());
+  return ZDL_OK;
+}
+
 static int link_insertion(zdl_ctx* c, zdl_links* out, const unsigned long long* call,
                           const unsigned long long* errc, const unsigned long long* first_rank) {
   const uint64_t SS = (uint64_t)c->rows * c->S;
-  if (SS <= MAP_CAP) {  // one kernel into mapped memory, one wait, the rank sort on the host
-    if (!c->h_ordmap) {
-      HIP_TRY(c, hipHostMalloc((void**)&c->h_ordmap, 16 + 32 * MAP_CAP, hipHostMallocMapped | hipHostMallocCoherent));
-      HIP_TRY(c, hipHostGetDevicePointer((void**)&c->d_ordmap, c->h_ordmap, 0));
+  if (SS <= MAP_CAP) {  // one kernel into mapped memory (queued by the put already when fresh), one wait
+    if (!(c->ordmap_fresh && call == c->call.p)) {
+      const int orc = ord_compact(c, call, errc, first_rank);
+      if (orc != ZDL_OK) return orc;
     }
-    hipLaunchKernelGGL(k_ord_compact, dim3(1), dim3(COMPACT_WG), ORD_COMPACT_LDS, c->stream, call, errc, first_rank,
-                       (uint32_t)SS, c->S, c->status.p, c->d_ordmap);
-    HIP_TRY(c, hipGetLastError());
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     put_times(c);
     const int rc = status_code(c, (uint32_t)c->h_ordmap[0]);
@@ -4272,6 +4312,7 @@ int zdl_add_links(zdl_ctx* c, const int32_t* parent, const int32_t* child, const
   HIP_TRY(c, hipGetLastError());
   if (c->ord) c->span_base += n;  // the links rank before anything put afterwards (ord_rank's layout)
   c->map_fresh = false;
+  c->ordmap_fresh = false;
   return zdl_sync(c);
 }
 
@@ -4322,6 +4363,7 @@ int zdl_table_import(zdl_ctx* c, const void* dev_call, const void* dev_err) {
   HIP_TRY(c, hipMemcpyAsync(c->call.p, dev_call, bytes, hipMemcpyDeviceToDevice, c->stream));
   HIP_TRY(c, hipMemcpyAsync(c->errc.p, dev_err, bytes, hipMemcpyDeviceToDevice, c->stream));
   c->map_fresh = false;
+  c->ordmap_fresh = false;
   return ZDL_OK;
 }
 
