@@ -198,42 +198,11 @@ __global__ void __launch_bounds__(RL_T) k_rl_cells(const uint32_t* __restrict__ 
   }
 }
 
-// The log's sort: rocprim's onesweep radix sort with RB bits a pass (the gfx950 default is 8:
-// four passes over C5's 28-bit keys). ZDL_SORT_BITS (A/B) picks 8, 10 or 11.
-#ifndef ZDL_LOGSORT_HB
-#define ZDL_LOGSORT_HB 1024  // A/B builds: the histogram kernel's block size and items per thread,
-#define ZDL_LOGSORT_HI 8     // then the sort passes'
-#define ZDL_LOGSORT_SB 1024
-#define ZDL_LOGSORT_SI 8
-#endif
-template <unsigned RB>
-using LogSortCfg = ::rocprim::radix_sort_config<
-    ::rocprim::default_config, ::rocprim::default_config,
-    ::rocprim::radix_sort_onesweep_config<::rocprim::kernel_config<ZDL_LOGSORT_HB, ZDL_LOGSORT_HI>,
-                                          ::rocprim::kernel_config<ZDL_LOGSORT_SB, ZDL_LOGSORT_SI>, RB,
-                                          ::rocprim::block_radix_rank_algorithm::match>>;
-int sort_bits() {
-  static const int b = [] {
-    const char* e = getenv("ZDL_SORT_BITS");
-    const int v = e ? atoi(e) : 8;
-    return v == 10 || v == 11 ? v : 8;
-  }();
-  return b;
-}
+// The log's sort: hipcub's radix sort (onesweep, 8-bit digits: four passes over C5's 28-bit keys;
+// rocprim onesweep configs with 10- and 11-bit digits, three passes, were measured and not kept)
 hipError_t sort_log(void* tmp, size_t& bytes, const uint32_t* in, uint32_t* out, uint64_t E, int key_bits,
                     hipStream_t s) {
-  switch (sort_bits()) {
-    case 10:
-      return ::rocprim::radix_sort_keys<LogSortCfg<10>>(tmp, bytes, in, out, (size_t)E, 0u, (unsigned)key_bits, s);
-    case 11:
-      return ::rocprim::radix_sort_keys<LogSortCfg<11>>(tmp, bytes, in, out, (size_t)E, 0u, (unsigned)key_bits, s);
-    default:
-#ifdef ZDL_LOGSORT_CFG8
-      return ::rocprim::radix_sort_keys<LogSortCfg<8>>(tmp, bytes, in, out, (size_t)E, 0u, (unsigned)key_bits, s);
-#else
-      return hipcub::DeviceRadixSort::SortKeys(tmp, bytes, in, out, (int)E, 0, key_bits, s);
-#endif
-  }
+  return hipcub::DeviceRadixSort::SortKeys(tmp, bytes, in, out, (int)E, 0, key_bits, s);
 }
 
 hipError_t scratch(SparseWork& w, size_t need) {
