@@ -229,3 +229,31 @@ def test_insertion_order_needs_the_flag_and_reset_clears_ranks():
     b = ctx.link(N.ZDL_ORDER_INSERTION)
     assert all(np.array_equal(x, y) for x, y in zip(a, b))
     ctx.close()
+
+
+def test_link_between_puts_and_after_add_links():
+    """The insertion-order compaction is queued at each put's end (round 6): a link after every
+    put sees every put so far, a second link without a put returns the same list, and a table
+    changed by zdl_add_links is compacted again (the put's compaction is stale then)."""
+    from zipkin_amd.columnar import concat_columns
+    w = synth.C2.scaled(30_000)
+    cols = synth.generate(w)
+    parts = list(_split(cols, 3))
+    ctx = N.Context(w.total_services, insertion_order=True)
+    try:
+        for k in range(1, 4):
+            ctx.put_spans(parts[k - 1])
+            got = ctx.link(N.ZDL_ORDER_INSERTION)
+            st, op, oc, on, oe = ref.link(concat_columns(parts[:k]), threads=8)
+            assert st == 0
+            exp = list(zip(op.tolist(), oc.tolist(), on.tolist(), oe.tolist()))
+            assert list(zip(*(a.tolist() for a in got))) == exp
+            again = ctx.link(N.ZDL_ORDER_INSERTION)
+            assert list(zip(*(a.tolist() for a in again))) == exp
+        p, c, n, e = (np.asarray(a[:5]) for a in got)
+        ctx.add_links(p, c, np.ones(5, np.int64), np.zeros(5, np.int64))
+        bumped = ctx.link(N.ZDL_ORDER_INSERTION)
+        want = [(a, b, x + (1 if i < 5 else 0), y) for i, (a, b, x, y) in enumerate(exp)]
+        assert list(zip(*(a.tolist() for a in bumped))) == want
+    finally:
+        ctx.close()
