@@ -3019,6 +3019,8 @@ static int put_spans_ungrouped(zdl_ctx* c, const zdl_span_cols* col, uint64_t n)
 struct zdl_store {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t cstream = nullptr;  // zdl_store_append: the columns the index does not read
+  hipEvent_t cev = nullptr;
   std::string err;
   uint64_t n = 0, cap = 0, n_alive = 0;
   DevBuf<uint64_t> id, pid, lo, hi;
@@ -3166,7 +3168,11 @@ extern "C" {
 zdl_store* zdl_store_create(int device) {
   zdl_store* st = new zdl_store();
   st->device = device;
-  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&st->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&st->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&st->cstream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&st->cev, hipEventDisableTiming) != hipSuccess) {
+    if (st->cstream) (void)hipStreamDestroy(st->cstream);
+    if (st->stream) (void)hipStreamDestroy(st->stream);
     g_create_error = "zdl_store_create: device init failed";
     delete st;
     return nullptr;
@@ -3182,6 +3188,9 @@ void zdl_store_destroy(zdl_store* st) {
   st->ip4.release(); st->ip6.release(); st->pf.release(); st->ts.release(); st->alive.release();
   st->sel.release(); st->sel_off.release();
   st->iw.release();
+  (void)hipStreamSynchronize(st->cstream);
+  (void)hipEventDestroy(st->cev);
+  (void)hipStreamDestroy(st->cstream);
   (void)hipStreamDestroy(st->stream);
   delete st;
 }
@@ -3227,33 +3236,42 @@ int zdl_store_append_ids(zdl_store* st, const zdl_span_cols* col, const uint64_t
     if (e == hipSuccess) st->cap = cap;
   }
   const uint64_t o = st->n;
-  if (e == hipSuccess) e = hipMemcpyAsync(st->id.p + o, col->id, n * 8, hipMemcpyDefault, s);
-  if (e == hipSuccess) e = hipMemcpyAsync(st->pid.p + o, col->parent_id, n * 8, hipMemcpyDefault, s);
+  // The trace index reads trace_lo and the timestamps only: they cross PCIe first, the index
+  // update (sort + merge) runs on the stream while the other columns cross on cstream.
   if (e == hipSuccess)
     e = col->trace_lo ? hipMemcpyAsync(st->lo.p + o, col->trace_lo, n * 8, hipMemcpyDefault, s)
                       : hipMemsetAsync(st->lo.p + o, 0, n * 8, s);
   if (e == hipSuccess)
-    e = trace_hi ? hipMemcpyAsync(st->hi.p + o, trace_hi, n * 8, hipMemcpyDefault, s)
-                 : hipMemsetAsync(st->hi.p + o, 0, n * 8, s);
-  if (e == hipSuccess) e = hipMemcpyAsync(st->lsvc.p + o, col->local_svc, n * 4, hipMemcpyDefault, s);
-  if (e == hipSuccess) e = hipMemcpyAsync(st->rsvc.p + o, col->remote_svc, n * 4, hipMemcpyDefault, s);
-  if (e == hipSuccess) e = hipMemcpyAsync(st->ip4.p + o, col->local_ip4, n * 4, hipMemcpyDefault, s);
-  if (e == hipSuccess) e = hipMemcpyAsync(st->ip6.p + o, col->local_ip6, n * 4, hipMemcpyDefault, s);
-  if (e == hipSuccess) e = hipMemcpyAsync(st->pf.p + o, col->port_flags, n * 4, hipMemcpyDefault, s);
-  if (e == hipSuccess)
     e = col->timestamp ? hipMemcpyAsync(st->ts.p + o, col->timestamp, n * 8, hipMemcpyDefault, s)
                        : hipMemsetAsync(st->ts.p + o, 0, n * 8, s);
-  // alive bytes: 1, | 2 for a 128-bit trace id (the strict grouping's width bit)
-  if (e == hipSuccess && trace_wide) e = hipMemcpyAsync(st->alive.p + o, trace_wide, n, hipMemcpyDefault, s);
-  if (e == hipSuccess) {
-    hipLaunchKernelGGL(k_alive_init, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, st->alive.p + o,
-                       trace_hi ? st->hi.p + o : nullptr, trace_wide ? 1 : 0, n);
-    e = hipGetLastError();
-  }
+  if (e == hipSuccess) e = hipEventRecord(st->cev, s);  // (and the growth's copies before it)
   // the resident trace index takes the batch in (sorted, merged: the TreeMap inserts of
   // InMemoryStorage.accept, IMS:156-181), so a query only filters and orders traces
   if (e == hipSuccess) e = zdl::index_update(st->iw, st->lo.p, st->ts.p, st->n + n, s);
-  if (e == hipSuccess) e = hipStreamSynchronize(s);  // the columns are borrowed for the call only
+  const hipStream_t cs = st->cstream;
+  if (e == hipSuccess) e = hipStreamWaitEvent(cs, st->cev, 0);
+  if (e == hipSuccess) e = hipMemcpyAsync(st->id.p + o, col->id, n * 8, hipMemcpyDefault, cs);
+  if (e == hipSuccess) e = hipMemcpyAsync(st->pid.p + o, col->parent_id, n * 8, hipMemcpyDefault, cs);
+  if (e == hipSuccess)
+    e = trace_hi ? hipMemcpyAsync(st->hi.p + o, trace_hi, n * 8, hipMemcpyDefault, cs)
+                 : hipMemsetAsync(st->hi.p + o, 0, n * 8, cs);
+  if (e == hipSuccess) e = hipMemcpyAsync(st->lsvc.p + o, col->local_svc, n * 4, hipMemcpyDefault, cs);
+  if (e == hipSuccess) e = hipMemcpyAsync(st->rsvc.p + o, col->remote_svc, n * 4, hipMemcpyDefault, cs);
+  if (e == hipSuccess) e = hipMemcpyAsync(st->ip4.p + o, col->local_ip4, n * 4, hipMemcpyDefault, cs);
+  if (e == hipSuccess) e = hipMemcpyAsync(st->ip6.p + o, col->local_ip6, n * 4, hipMemcpyDefault, cs);
+  if (e == hipSuccess) e = hipMemcpyAsync(st->pf.p + o, col->port_flags, n * 4, hipMemcpyDefault, cs);
+  // alive bytes: 1, | 2 for a 128-bit trace id (the strict grouping's width bit)
+  if (e == hipSuccess && trace_wide) e = hipMemcpyAsync(st->alive.p + o, trace_wide, n, hipMemcpyDefault, cs);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_alive_init, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, cs, st->alive.p + o,
+                       trace_hi ? st->hi.p + o : nullptr, trace_wide ? 1 : 0, n);
+    e = hipGetLastError();
+  }
+  {  // the columns are borrowed for the call only: both streams finish before it returns
+    const hipError_t e1 = hipStreamSynchronize(cs);
+    const hipError_t e2 = hipStreamSynchronize(s);
+    if (e == hipSuccess) e = e1 != hipSuccess ? e1 : e2;
+  }
   if (e != hipSuccess) return store_hip_fail(st, e, "zdl_store_append");
   st->n += n;
   st->n_alive += n;
