@@ -8,7 +8,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 O=gpurun_out; mkdir -p $O
 CFG=${1:-c2}; ROUNDS=${2:-2}
-B="bench.py --config $CFG --no-c3-job --steps 12 --warmup 3 --no-cpu-baseline --no-h2d --no-proto3 --no-json --no-store --no-mysql-rows --no-insertion-order --no-parity --no-c5 --no-traffic --no-put-trace"
+B="bench.py --config $CFG --no-c3-job --steps 12 --warmup 3 --warm-ms 100 --no-cpu-baseline --no-h2d --no-proto3 --no-json --no-store --no-mysql-rows --no-insertion-order --no-parity --no-c5 --no-traffic --no-put-trace"
 j() { tail -1 $1 | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); c=d["config"]; r=c.get("log_reduce"); print(round(c["kernel_ms"]["k_link"]*1e3,1), round(d["ms_per_step"]*1e3,1), "reduce", round(r["ms"]*1e3,1) if r else "-", r["entries"] if r else "")'; }
 j5() { tail -1 $1 | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(round(d["ms_per_step"],3), round(d["ms_per_step_serial"],3), d["parity"], {k: round(v["ms"],3) for k,v in d["phases"].items()})'; }
 for rep in $(seq $ROUNDS); do
