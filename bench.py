@@ -815,7 +815,8 @@ def h2d_leg(cols, S, device, reps=3):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=200,
+                    help="timed steps (the pipeline of two steps in flight fills and drains once per leg: ~5 %% of 20 steps)")
     ap.add_argument("--warmup", type=int, default=20, help="untimed steps before the timed ones")
     ap.add_argument("--warm-ms", type=float, default=200.0,
                     help="after the --warmup steps, more untimed steps until the warm-up has lasted this long "
