@@ -377,7 +377,7 @@ def _small_bytes(sizes, n_traces):
     return BYTES_PER_SPAN * int(sizes[sizes <= 64].sum()) + BYTES_PER_TRACE * (n_traces + 1)
 
 
-def c5_leg(device, steps=16, parity=True, threads=16, host_threads=2, warm_ms=200.0):
+def c5_leg(device, steps=48, parity=True, threads=16, host_threads=2, warm_ms=200.0):
     """BASELINE.json configs[4] (C5: 10 000 services, Zipf(1.1), depth 64, fan-out <= 1000,
     Pareto(1.2) trace sizes clipped to [1, 200 000]: 81.1M spans / 16M traces) on one GPU, a
     sparse context (the link list sorted by cell, no S x S table). One step = reset, put of the
